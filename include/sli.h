@@ -1,0 +1,170 @@
+/*
+ * sli.h — the C ABI of the MI355X-native decode path (libsli.so).
+ *
+ * Plain pointers, sizes and status codes only (no torch or HIP types in any signature; a stream is an
+ * opaque void* that is a hipStream_t, NULL = the default stream). Device pointers are HIP device
+ * memory on the current device. Every entry point returns SLI_OK (0) or an sli_status code; the text
+ * of the last error on the calling thread is available from sli_last_error().
+ *
+ * Two layers:
+ *  (1) kernel level — one entry point per reference launcher in include/kernel/cuda/ (*.cuh); the C++
+ *      drop-in op:: layer (include/op/, simplellminference_amd/csrc/host/) unpacks mem::Tensor and
+ *      calls these;
+ *  (2) model level — the whole LlamaModel decode step (source/model/model.cpp:40-187) as one fused,
+ *      graph-captured HIP step per token, optionally tensor-parallel over RCCL.
+ * Reference citations are /root/reference paths.
+ */
+#ifndef SLI_H_
+#define SLI_H_
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    SLI_OK = 0,
+    SLI_ERR_ARG = 1,    /* null pointer / bad enum / bad scalar */
+    SLI_ERR_SHAPE = 2,  /* tensor dimensions inconsistent (reference: LOG("Tensor with Wrong Dim!")) */
+    SLI_ERR_RANGE = 3,  /* token or position out of range (reference: emb_kernel.cpp:10) */
+    SLI_ERR_HIP = 4,    /* HIP runtime error */
+    SLI_ERR_NOMEM = 5,  /* device allocation failed */
+    SLI_ERR_COMM = 6,   /* RCCL error */
+    SLI_ERR_STATE = 7   /* call not valid in the object's current state */
+} sli_status;
+
+typedef enum { SLI_DT_F32 = 0, SLI_DT_F16 = 1, SLI_DT_I8 = 2 } sli_dtype;
+
+typedef void* sli_stream_t;
+
+int sli_version(void);
+const char* sli_status_str(int status);
+const char* sli_last_error(void);
+
+/* ---------------------------------------------------------------- device helpers */
+int sli_device_count(int* n);
+int sli_set_device(int device);
+int sli_malloc(void** ptr, size_t bytes);
+int sli_free(void* ptr);
+int sli_memset(void* ptr, int value, size_t bytes, sli_stream_t stream);
+int sli_memcpy_h2d(void* dst, const void* src, size_t bytes, sli_stream_t stream);
+int sli_memcpy_d2h(void* dst, const void* src, size_t bytes, sli_stream_t stream);
+int sli_memcpy_d2d(void* dst, const void* src, size_t bytes, sli_stream_t stream);
+int sli_stream_create(sli_stream_t* out);
+int sli_stream_destroy(sli_stream_t stream);
+int sli_stream_sync(sli_stream_t stream);
+
+/* ---------------------------------------------------------------- kernel level
+ * Each replaces one reference CUDA launcher; semantics follow the reference CPU kernel (the oracle). */
+
+/* kernel::matmul_kernel_cuda (include/kernel/cuda/matmul_kernel.cuh:6-7; CPU semantics
+ * source/kernel/cpu/matmul_kernel.cpp:5-28): y[r] = scale * sum_c x[c] * W[r][c]; W row-major
+ * [rows][cols] in w_dtype; w_row_scale[rows] multiplies each row for SLI_DT_I8 (NULL otherwise). */
+int sli_matmul(const float* x, const void* w, int w_dtype, const float* w_row_scale, float* y, int32_t rows,
+               int32_t cols, float scale, sli_stream_t stream);
+
+/* kernel::rmsnorm_kernel_cuda (rms_kernel.cuh:6-7; CPU rms_kernel.cpp:5-23): y = x / sqrt(mean(x^2)+eps) * w.
+ * Single-workgroup reduction: no atomics, no per-call allocation (the reference allocates + memsets a
+ * {1} tensor per call and races across blocks, rms_kernel.cu:29-33,48-51). */
+int sli_rmsnorm(const float* x, const float* w, float* y, int32_t dim, float eps, sli_stream_t stream);
+
+/* kernel::rope_cache_cal_cuda (rope_kernel.cuh:5-6; CPU rope_kernel.cpp:4-19): the fp32 sin/cos table
+ * [max_seq_len][head_dim/2] is computed on the host with libm powf/sinf/cosf (bit-identical to the
+ * reference CPU table) and copied to sin_dev / cos_dev. */
+int sli_rope_cache(int32_t head_dim, int32_t max_seq_len, float* sin_dev, float* cos_dev, float theta,
+                   sli_stream_t stream);
+
+/* kernel::rope_kernel_cuda (rope_kernel.cuh:7-8; CPU rope_kernel.cpp:22-41): rotate-half RoPE of q
+ * (q_dim) and k (k_dim) at position pos_dev ? *pos_dev : pos. k is rotated over k_dim only. */
+int sli_rope(float* q, float* k, int32_t pos, const int32_t* pos_dev, const float* sin_dev, const float* cos_dev,
+             int32_t q_dim, int32_t k_dim, int32_t head_dim, sli_stream_t stream);
+
+/* kernel::mha_kernel_cuda (mha_kernel.cuh:6-21; CPU mha_kernel.cpp:36-77): decode attention for one
+ * layer at position pos over a KV cache in REFERENCE layout [L][T][KV] (fp32 or fp16). Split-context
+ * flash-decoding: needs sli_mha_workspace_bytes() of device scratch (the reference's {hd,T} score
+ * buffer is not needed). */
+size_t sli_mha_workspace_bytes(int32_t max_seq_len, int32_t n_heads, int32_t head_dim);
+int sli_mha(const float* q, const void* kcache, const void* vcache, int kv_dtype, float* out, int32_t layer,
+            int32_t pos, int32_t max_seq_len, int32_t head_dim, int32_t n_heads, int32_t n_kv_heads,
+            void* workspace, size_t workspace_bytes, sli_stream_t stream);
+
+/* softmax_kernel_cpu (mha_kernel.cpp:7-20) as a standalone in-place op over n floats. */
+int sli_softmax(float* x, int32_t n, sli_stream_t stream);
+
+/* kernel::swiglu_kernel_cuda (swiglu_kernel.cuh:5; CPU swiglu_kernel.cpp:5-15): out = sigmoid(gate)*up
+ * (the reference variant; see sli_model_config.act_mode for SiLU). */
+int sli_swiglu(const float* up, const float* gate, float* out, int32_t n, sli_stream_t stream);
+
+/* kernel::add_kernel_cuda (add_kernel.cuh:6; CPU add_kernel.cpp:5-14): out = a + b. */
+int sli_add(const float* a, const float* b, float* out, int32_t n, sli_stream_t stream);
+
+/* kernel::emb_kernel_cuda (emb_kernel.cuh:6-7; CPU emb_kernel.cpp:4-21): out = table[token] (row
+ * dequantised for SLI_DT_I8 with row_scale). token = token_dev ? *token_dev : token. Returns
+ * SLI_ERR_RANGE for a host token outside [0, vocab); a device token outside that range writes zeros. */
+int sli_embedding(int32_t token, const int32_t* token_dev, const void* table, int dtype, const float* row_scale,
+                  float* out, int32_t vocab, int32_t dim, sli_stream_t stream);
+
+/* argmaxLayer::forward (source/op/argmax.cpp:7-17) on device: first index of the maximum. */
+int sli_argmax(const float* logits, int32_t n, int32_t* out_dev, sli_stream_t stream);
+
+/* ---------------------------------------------------------------- model level */
+typedef struct {
+    int32_t vocab, dim, n_heads, n_kv_heads, head_dim, ffn, n_layers, max_len;
+    float eps, theta;
+    int32_t w_dtype;  /* SLI_DT_F32 / SLI_DT_F16 / SLI_DT_I8 (per-row symmetric) */
+    int32_t kv_dtype; /* SLI_DT_F32 / SLI_DT_F16 */
+    int32_t act_mode; /* 0: reference sigmoid(gate)*up (swiglu_kernel.cpp:12-13); 1: SiLU(gate)*up */
+    int32_t tp_rank, tp_size;
+    int32_t device;
+} sli_model_config;
+
+typedef struct sli_model sli_model;
+
+/* RCCL unique id for tensor parallelism (broadcast it from rank 0 with any host transport). */
+int sli_comm_id_bytes(void);
+int sli_comm_get_id(void* out);
+
+int sli_model_create(const sli_model_config* cfg, const void* comm_id, sli_model** out);
+int sli_model_destroy(sli_model* m);
+/* Seeded synthetic weights (include/sli_synth.h), generated on device in this rank's shard. */
+int sli_model_init_synthetic(sli_model* m, uint32_t seed);
+/* Place one full, unsharded, reference-layout fp32 tensor (kind/index from sli_synth.h). */
+int sli_model_set_weight(sli_model* m, int32_t kind, int32_t index, const float* host, int64_t n);
+/* Load the reference's flat fp32 weight file (model.cpp:204-245 read, :336-469 layout). */
+int sli_model_load_flat(sli_model* m, const char* path);
+/* Zero the KV cache and the decode state. */
+int sli_model_reset(sli_model* m);
+/* Fill K/V rows [0, upto) of every layer with the synthetic N(0,1) values (bench context fill). */
+int sli_model_fill_kv_synthetic(sli_model* m, uint32_t seed, int32_t upto);
+/* Decode state: the token fed at position pos. advance=1: after each step pos += 1 and the next token
+ * is the teacher-forced prompt id or the greedy argmax (model.cpp:157-183); advance=0: the step is
+ * idempotent (recomputes the same position; the bench mode). */
+int sli_model_set_state(sli_model* m, int32_t token, int32_t pos, int32_t advance);
+int sli_model_set_prompt(sli_model* m, const int32_t* ids, int32_t n);
+int sli_model_get_state(sli_model* m, int32_t* pos, int32_t* token, int32_t* last_argmax, int32_t* error);
+/* One decode step (hipGraph replay; captured on first use). Asynchronous on the model's stream. */
+int sli_model_step(sli_model* m);
+int sli_model_sync(sli_model* m);
+/* logits of the last step: this rank's vocab shard [vocab_lo, vocab_lo+n). */
+int sli_model_get_logits(sli_model* m, float* host, int32_t n, int32_t* vocab_lo);
+/* LlamaModel::predict on token ids: tokens_out[t] = token fed at position t; logits_out optional
+ * [max_length][local vocab]. */
+int sli_model_predict(sli_model* m, const int32_t* prompt, int32_t n_prompt, int32_t max_length,
+                      int32_t* tokens_out, float* logits_out);
+/* Copy one layer's K (which=0) or V (which=1) cache, positions [0, upto), to host as fp32 in reference
+ * layout [upto][KV_local]. */
+int sli_model_get_kv(sli_model* m, int32_t layer, int32_t which, int32_t upto, float* host);
+int sli_model_stream(sli_model* m, sli_stream_t* out);
+/* Algorithmic HBM bytes of one step on this rank (weights, KV at the current position) — SURVEY.md §8(d). */
+int sli_model_step_bytes(sli_model* m, double* weight_bytes, double* kv_bytes);
+/* Roofline probe: replays the step's weight-streaming (GEMV) kernels `iters` times between HIP events
+ * on the model's stream; returns mean device time per GEMV launch, algorithmic bytes per launch and
+ * the launches per step. */
+int sli_model_time_gemv(sli_model* m, int32_t iters, double* avg_us, double* bytes_per_launch,
+                        int32_t* launches_per_step);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

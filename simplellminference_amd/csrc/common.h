@@ -1,0 +1,142 @@
+// common.h — shared HIP helpers for the gfx950 decode path (wave64 reductions, 16-byte vector loads,
+// error plumbing for the C ABI).
+#pragma once
+#include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/sli.h"
+
+namespace sli {
+
+constexpr int kWave = 64;  // CDNA wavefront; never 32 (MI355X_MICROARCH.md "wave = 64 not 32")
+
+// ---------------------------------------------------------------- error plumbing (host)
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+int hip_fail(hipError_t e, const char* what);
+
+#define SLI_HIP(expr)                                         \
+    do {                                                      \
+        hipError_t e_ = (expr);                               \
+        if (e_ != hipSuccess) return ::sli::hip_fail(e_, #expr); \
+    } while (0)
+
+#define SLI_CHECK(cond, code, msg)                        \
+    do {                                                  \
+        if (!(cond)) return ::sli::fail((code), (msg));   \
+    } while (0)
+
+inline hipStream_t as_stream(sli_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---------------------------------------------------------------- device helpers
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
+    return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+    return v;
+}
+
+// sum over groups of `width` consecutive lanes (width a power of two <= 64)
+template <int WIDTH>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+    for (int o = WIDTH / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
+    return v;
+}
+
+// 16-byte loads. NT = non-temporal (streamed-once weights: MI355X_MICROARCH.md "nt-weights").
+template <bool NT>
+__device__ __forceinline__ u32x4 load16(const void* p) {
+    if constexpr (NT) {
+        return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    } else {
+        return *reinterpret_cast<const u32x4*>(p);
+    }
+}
+
+// element types of a 16-byte vector
+template <typename T>
+struct Vec16;
+template <>
+struct Vec16<float> {
+    static constexpr int N = 4;
+    __device__ __forceinline__ static void unpack(const u32x4& v, float* o) {
+        o[0] = __uint_as_float(v.x);
+        o[1] = __uint_as_float(v.y);
+        o[2] = __uint_as_float(v.z);
+        o[3] = __uint_as_float(v.w);
+    }
+};
+template <>
+struct Vec16<__half> {
+    static constexpr int N = 8;
+    __device__ __forceinline__ static void unpack(const u32x4& v, float* o) {
+        unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            __half2 h = *reinterpret_cast<const __half2*>(&w[i]);
+            float2 f = __half22float2(h);
+            o[2 * i] = f.x;
+            o[2 * i + 1] = f.y;
+        }
+    }
+};
+template <>
+struct Vec16<int8_t> {
+    static constexpr int N = 16;
+    __device__ __forceinline__ static void unpack(const u32x4& v, float* o) {
+        unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+            for (int b = 0; b < 4; ++b) o[4 * i + b] = (float)(int)(int8_t)((w[i] >> (8 * b)) & 0xFFu);
+        }
+    }
+};
+
+template <typename T>
+__device__ __forceinline__ float to_f32(T v);
+template <>
+__device__ __forceinline__ float to_f32<float>(float v) { return v; }
+template <>
+__device__ __forceinline__ float to_f32<__half>(__half v) { return __half2float(v); }
+template <>
+__device__ __forceinline__ float to_f32<int8_t>(int8_t v) { return (float)(int)v; }
+
+template <typename T>
+__device__ __forceinline__ T from_f32(float v);
+template <>
+__device__ __forceinline__ float from_f32<float>(float v) { return v; }
+template <>
+__device__ __forceinline__ __half from_f32<__half>(float v) { return __float2half_rn(v); }
+
+// Orderable 64-bit argmax key: larger value wins; equal values -> lower index wins (std::max_element's
+// first-max rule, source/op/argmax.cpp:11). Key 0 is below every real key.
+__device__ __forceinline__ unsigned long long argmax_key(float v, unsigned idx) {
+    unsigned u = __float_as_uint(v);
+    unsigned ord = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+    return ((unsigned long long)ord << 32) | (unsigned long long)(0xFFFFFFFFu - idx);
+}
+__device__ __forceinline__ unsigned argmax_key_index(unsigned long long k) {
+    return 0xFFFFFFFFu - (unsigned)(k & 0xFFFFFFFFull);
+}
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        unsigned long long w = __shfl_xor(v, o, kWave);
+        v = w > v ? w : v;
+    }
+    return v;
+}
+
+}  // namespace sli

@@ -1,0 +1,803 @@
+// engine.hip — the model-level C ABI (include/sli.h): LlamaModel's decode step
+// (source/model/model.cpp:40-140) and decode loop (:142-187) as a fused, graph-captured HIP step,
+// sharded Megatron-style over tp_size ranks (one process per GPU) with RCCL all-reduces.
+//
+// Per layer, five streaming launches replace the reference's ~18:
+//   1. RMSNorm ⊕ [wq;wk;wv] GEMV ⊕ RoPE ⊕ K/V cache write        (model.cpp:52-67)
+//   2. attention partials (split context)   3. combine           (model.cpp:70-78)
+//   4. wo GEMV ⊕ residual add  [+ all-reduce under TP]           (model.cpp:80-90)
+//   5. RMSNorm ⊕ [gate;up] GEMV ⊕ SwiGLU                         (model.cpp:93-115)
+//   6. down GEMV ⊕ residual add [+ all-reduce under TP]          (model.cpp:118-128)
+// then RMSNorm ⊕ tied LM head ⊕ argmax keys, key reduce [+ all-reduce max], and a one-thread finalize
+// that advances the on-device position/token (teacher forcing or greedy, model.cpp:157-183).
+// Token and position live in device memory, so one captured hipGraph serves every step.
+#include <fcntl.h>
+#include <rccl/rccl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "../../include/sli_synth.h"
+#include "attention.h"
+#include "common.h"
+#include "gemv.h"
+#include "ops_internal.h"
+#include "rope_table.h"
+
+namespace sli {
+
+struct DevState {
+    int32_t pos;          // position of the token being fed
+    int32_t token;        // token fed at pos
+    int32_t n_forced;     // prompt length (teacher forcing while pos < n_forced)
+    int32_t last_argmax;  // greedy argmax of the last step's logits
+    int32_t advance;      // 1: finalize advances pos/token; 0: idempotent step (bench)
+    int32_t error;
+    unsigned long long key;  // argmax key of the last step (0 between steps)
+};
+
+struct LayerW {
+    void* qkv = nullptr;   // [(hq + 2 hkv) hd][D]
+    float* qkv_s = nullptr;
+    void* wo = nullptr;    // [D][hq hd]   (column slice of wo, re-laid contiguous)
+    float* wo_s = nullptr;
+    void* gu = nullptr;    // [2 Il][D]    (gate rows then up rows)
+    float* gu_s = nullptr;
+    void* down = nullptr;  // [D][Il]      (column slice of down)
+    float* down_s = nullptr;
+};
+
+}  // namespace sli
+
+struct sli_model {
+    sli_model_config c{};
+    hipStream_t stream = nullptr;
+    ncclComm_t comm = nullptr;
+    // local (this rank's) geometry
+    int D = 0, L = 0, T = 0, V = 0, hd = 0, hq = 0, hkv = 0, Il = 0;
+    int v_lo = 0, v_n = 0;
+    size_t wbytes = 4, kvbytes = 4;
+    // device buffers
+    void* emb = nullptr;
+    float* emb_s = nullptr;
+    float* norms = nullptr;
+    std::vector<sli::LayerW> layers;
+    void* kc = nullptr;
+    void* vc = nullptr;
+    float *x = nullptr, *xpart = nullptr, *q = nullptr, *attn = nullptr, *act = nullptr, *logits = nullptr;
+    float* part = nullptr;
+    float *sin_t = nullptr, *cos_t = nullptr;
+    unsigned long long* keys = nullptr;
+    sli::DevState* st = nullptr;
+    int32_t* prompt = nullptr;
+    int32_t* hist = nullptr;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t graph_exec = nullptr;
+    std::vector<void*> allocs;
+};
+
+namespace sli {
+
+static int model_alloc(sli_model* m, void** p, size_t bytes) {
+    hipError_t e = hipMalloc(p, bytes ? bytes : 16);
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc");
+    m->allocs.push_back(*p);
+    return SLI_OK;
+}
+
+#define SLI_TRY(expr)                   \
+    do {                                \
+        int rc_ = (expr);               \
+        if (rc_ != SLI_OK) return rc_;  \
+    } while (0)
+
+#define SLI_NCCL(expr)                                                                          \
+    do {                                                                                        \
+        ncclResult_t r_ = (expr);                                                               \
+        if (r_ != ncclSuccess) return fail(SLI_ERR_COMM, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+// ---------------------------------------------------------------- weight placement
+struct SrcSynth {
+    uint32_t seed, stream;
+    float c, offset;
+    __device__ float operator()(uint64_t idx) const {
+        const float v = __fmul_rn((float)sli_rng_ih4(seed, stream, idx), c);
+        return offset != 0.0f ? __fadd_rn(offset, v) : v;  // sli_synth.h: one mul, one add, no FMA
+    }
+};
+
+struct SrcBuf {
+    const float* p;
+    __device__ float operator()(uint64_t idx) const { return p[idx]; }
+};
+
+// Copy the [row_lo, row_lo+nrows) x [col_lo, col_lo+ncols) window of a full [*, full_cols] fp32
+// tensor into dst (row stride ncols) as T. int8: per-row symmetric scale over the FULL row
+// (max|w|/127, q = rint(w/s)), so column shards share the unsharded quantisation.
+template <typename T, class Src>
+__global__ void __launch_bounds__(256) place_kernel(T* dst, float* dst_scale, int nrows, int ncols, int row_lo,
+                                                    int col_lo, int full_cols, Src src) {
+    __shared__ float red[4];
+    for (int r = blockIdx.x; r < nrows; r += gridDim.x) {
+        const uint64_t base = (uint64_t)(row_lo + r) * (uint64_t)full_cols;
+        if constexpr (sizeof(T) == 1) {
+            float mx = 0.0f;
+            for (int c = threadIdx.x; c < full_cols; c += blockDim.x) mx = fmaxf(mx, fabsf(src(base + c)));
+            mx = wave_max(mx);
+            if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+            __syncthreads();
+            mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+            __syncthreads();
+            const float s = __fdiv_rn(mx, 127.0f);
+            if (threadIdx.x == 0) dst_scale[r] = s;
+            for (int c = threadIdx.x; c < ncols; c += blockDim.x) {
+                float q = s > 0.0f ? rintf(__fdiv_rn(src(base + col_lo + c), s)) : 0.0f;
+                q = fminf(127.0f, fmaxf(-127.0f, q));
+                dst[(size_t)r * ncols + c] = (T)(int)q;
+            }
+        } else {
+            for (int c = threadIdx.x; c < ncols; c += blockDim.x)
+                dst[(size_t)r * ncols + c] = from_f32<T>(src(base + col_lo + c));
+        }
+    }
+}
+
+template <class Src>
+static int place(sli_model* m, void* dst, float* dst_scale, int nrows, int ncols, int row_lo, int col_lo, int full_cols,
+                 const Src& src) {
+    const int blocks = std::min(nrows, 4096);
+    hipStream_t s = m->stream;
+    switch (m->c.w_dtype) {
+        case SLI_DT_F32:
+            hipLaunchKernelGGL((place_kernel<float, Src>), dim3(blocks), dim3(256), 0, s, (float*)dst, dst_scale, nrows,
+                               ncols, row_lo, col_lo, full_cols, src);
+            break;
+        case SLI_DT_F16:
+            hipLaunchKernelGGL((place_kernel<__half, Src>), dim3(blocks), dim3(256), 0, s, (__half*)dst, dst_scale,
+                               nrows, ncols, row_lo, col_lo, full_cols, src);
+            break;
+        default:
+            hipLaunchKernelGGL((place_kernel<int8_t, Src>), dim3(blocks), dim3(256), 0, s, (int8_t*)dst, dst_scale,
+                               nrows, ncols, row_lo, col_lo, full_cols, src);
+    }
+    SLI_HIP(hipGetLastError());
+    return SLI_OK;
+}
+
+template <class Src>
+static int place_f32(sli_model* m, float* dst, int n, const Src& src) {
+    hipLaunchKernelGGL((place_kernel<float, Src>), dim3(1), dim3(256), 0, m->stream, dst, nullptr, 1, n, 0, 0, n, src);
+    SLI_HIP(hipGetLastError());
+    return SLI_OK;
+}
+
+static char* wptr(void* base, size_t elem_bytes, size_t elems) { return (char*)base + elem_bytes * elems; }
+
+// Place one full reference tensor (kind, index) from `src` into this rank's shard(s).
+template <class Src>
+static int place_tensor(sli_model* m, int kind, int index, const Src& src) {
+    const int D = m->D, hd = m->hd, r = m->c.tp_rank;
+    const int Ifull = m->c.ffn;
+    const size_t wb = m->wbytes;
+    if (kind == SLI_T_EMB) return place(m, m->emb, m->emb_s, m->V, D, 0, 0, D, src);
+    if (kind == SLI_T_NORM) {
+        if (index < 0 || index > 2 * m->L) return fail(SLI_ERR_RANGE, "norm index");
+        return place_f32(m, m->norms + (size_t)index * D, D, src);
+    }
+    if (index < 0 || index >= m->L) return fail(SLI_ERR_RANGE, "layer index");
+    LayerW& w = m->layers[index];
+    const int qr = m->hq * hd, kr = m->hkv * hd;
+    switch (kind) {
+        case SLI_T_WQ:
+            return place(m, w.qkv, w.qkv_s, qr, D, r * qr, 0, D, src);
+        case SLI_T_WK:
+            return place(m, wptr(w.qkv, wb, (size_t)qr * D), w.qkv_s ? w.qkv_s + qr : nullptr, kr, D, r * kr, 0, D,
+                         src);
+        case SLI_T_WV:
+            return place(m, wptr(w.qkv, wb, (size_t)(qr + kr) * D), w.qkv_s ? w.qkv_s + qr + kr : nullptr, kr, D,
+                         r * kr, 0, D, src);
+        case SLI_T_WO:
+            return place(m, w.wo, w.wo_s, D, qr, 0, r * qr, D, src);
+        case SLI_T_GATE:
+            return place(m, w.gu, w.gu_s, m->Il, D, r * m->Il, 0, D, src);
+        case SLI_T_UP:
+            return place(m, wptr(w.gu, wb, (size_t)m->Il * D), w.gu_s ? w.gu_s + m->Il : nullptr, m->Il, D,
+                         r * m->Il, 0, D, src);
+        case SLI_T_DOWN:
+            return place(m, w.down, w.down_s, D, m->Il, 0, r * m->Il, Ifull, src);
+        default:
+            return fail(SLI_ERR_ARG, "unknown tensor kind");
+    }
+}
+
+static int64_t tensor_elems(const sli_model* m, int kind) {
+    const int64_t D = m->c.dim, KV = (int64_t)m->c.n_kv_heads * m->c.head_dim, I = m->c.ffn, V = m->c.vocab;
+    switch (kind) {
+        case SLI_T_EMB: return V * D;
+        case SLI_T_NORM: return D;
+        case SLI_T_WQ: case SLI_T_WO: return D * D;
+        case SLI_T_WK: case SLI_T_WV: return KV * D;
+        case SLI_T_UP: case SLI_T_GATE: case SLI_T_DOWN: return I * D;
+        default: return -1;
+    }
+}
+
+static float synth_c(const sli_model* m, int kind) {
+    switch (kind) {
+        case SLI_T_EMB: return SLI_SYNTH_C(0.02);
+        case SLI_T_NORM: return SLI_SYNTH_C(0.1);
+        case SLI_T_DOWN: return SLI_SYNTH_C(1.0 / std::sqrt((double)m->c.ffn));
+        default: return SLI_SYNTH_C(1.0 / std::sqrt((double)m->c.dim));
+    }
+}
+
+// ---------------------------------------------------------------- small kernels of the step
+__global__ void keyreduce_kernel(const unsigned long long* __restrict__ keys, int n, DevState* st) {
+    unsigned long long b = 0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) b = keys[i] > b ? keys[i] : b;
+    b = wave_max_u64(b);
+    __shared__ unsigned long long red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = b;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) b = red[w] > b ? red[w] : b;
+        st->key = red[0] > b ? red[0] : b;
+    }
+}
+
+// model.cpp:157-183: next position; teacher-forced prompt token while inside the prompt, else greedy.
+__global__ void finalize_kernel(DevState* st, const int32_t* __restrict__ prompt, int32_t* hist, int T) {
+    const unsigned long long k = st->key;
+    const int next = (int)argmax_key_index(k);
+    st->last_argmax = next;
+    st->key = 0;
+    if (st->advance) {
+        const int p = st->pos + 1;
+        if (p < T) {
+            st->pos = p;
+            st->token = p < st->n_forced ? prompt[p] : next;
+            hist[p] = st->token;
+        }
+    }
+}
+
+template <typename KT>
+__global__ void fill_kv_kernel(KT* kc, KT* vc, int L, int hkv, int T, int hd, int upto, int kv_full, int head_lo,
+                               uint32_t seed, float c) {
+    const uint64_t n = (uint64_t)L * hkv * upto * hd;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const int d = (int)(i % hd);
+        uint64_t rest = i / hd;
+        const int t = (int)(rest % upto);
+        rest /= upto;
+        const int h = (int)(rest % hkv);
+        const int l = (int)(rest / hkv);
+        const uint64_t idx = (uint64_t)t * kv_full + (uint64_t)(head_lo + h) * hd + d;  // reference layout index
+        const size_t off = (((size_t)l * hkv + h) * T + t) * hd + d;
+        kc[off] = from_f32<KT>(__fmul_rn((float)sli_rng_ih4(seed, sli_stream_id(SLI_T_KCACHE, l), idx), c));
+        vc[off] = from_f32<KT>(__fmul_rn((float)sli_rng_ih4(seed, sli_stream_id(SLI_T_VCACHE, l), idx), c));
+    }
+}
+
+template <typename KT>
+__global__ void get_kv_kernel(const KT* __restrict__ cache, float* out, int hkv, int T, int hd, int upto) {
+    const int n = upto * hkv * hd;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int d = i % hd, h = (i / hd) % hkv, t = i / (hd * hkv);
+        out[i] = to_f32(cache[((size_t)h * T + t) * hd + d]);
+    }
+}
+
+// ---------------------------------------------------------------- the step
+template <typename WT, typename KT>
+struct StepRecorder {
+    static constexpr bool NT = true;  // streamed-once weights: non-temporal loads
+    static int gemv_qkv(sli_model* m, int l) {
+        const LayerW& w = m->layers[l];
+        GemvIn in{m->x, m->norms + (size_t)(2 * l) * m->D, m->c.eps, m->D};
+        KT* kc = (KT*)m->kc + (size_t)l * m->hkv * m->T * m->hd;
+        KT* vc = (KT*)m->vc + (size_t)l * m->hkv * m->T * m->hd;
+        EpiQKV<KT> e{m->q, kc, vc, w.qkv_s, &m->st->pos, m->sin_t, m->cos_t, m->hq, m->hkv, m->hd, m->T};
+        SLI_HIP((launch_gemv<WT, 4, 4, NT>((const WT*)w.qkv, in, e, (m->hq + 2 * m->hkv) * (m->hd / 4), m->stream)));
+        return SLI_OK;
+    }
+    static int gemv_wo(sli_model* m, int l) {
+        const LayerW& w = m->layers[l];
+        const bool tp = m->c.tp_size > 1;
+        GemvIn in{m->attn, nullptr, 0.0f, m->hq * m->hd};
+        EpiStore<2> e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, w.wo_s, 1.0f, m->D};
+        SLI_HIP((launch_gemv<WT, 2, 8, NT>((const WT*)w.wo, in, e, (m->D + 1) / 2, m->stream)));
+        return SLI_OK;
+    }
+    static int gemv_gu(sli_model* m, int l) {
+        const LayerW& w = m->layers[l];
+        GemvIn in{m->x, m->norms + (size_t)(2 * l + 1) * m->D, m->c.eps, m->D};
+        EpiSwiGLU e{m->act, w.gu_s, m->Il, m->c.act_mode};
+        SLI_HIP((launch_gemv<WT, 4, 4, NT>((const WT*)w.gu, in, e, m->Il / 2, m->stream)));
+        return SLI_OK;
+    }
+    static int gemv_down(sli_model* m, int l) {
+        const LayerW& w = m->layers[l];
+        const bool tp = m->c.tp_size > 1;
+        GemvIn in{m->act, nullptr, 0.0f, m->Il};
+        EpiStore<2> e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, w.down_s, 1.0f, m->D};
+        SLI_HIP((launch_gemv<WT, 2, 8, NT>((const WT*)w.down, in, e, (m->D + 1) / 2, m->stream)));
+        return SLI_OK;
+    }
+    static int lm_head_blocks(sli_model* m) { return gemv_blocks((m->v_n + 1) / 2); }
+    static int gemv_lm(sli_model* m) {
+        GemvIn in{m->x, m->norms + (size_t)(2 * m->L) * m->D, m->c.eps, m->D};
+        EpiLogits<2> e{m->logits, m->keys, m->emb_s ? m->emb_s + m->v_lo : nullptr, m->v_n, m->v_lo, 0ull};
+        const WT* w = (const WT*)m->emb + (size_t)m->v_lo * m->D;
+        SLI_HIP((launch_gemv<WT, 2, 8, NT>(w, in, e, (m->v_n + 1) / 2, m->stream)));
+        return SLI_OK;
+    }
+    static int allreduce_x(sli_model* m) {
+        if (m->c.tp_size > 1) SLI_NCCL(ncclAllReduce(m->xpart, m->x, m->D, ncclFloat32, ncclSum, m->comm, m->stream));
+        return SLI_OK;
+    }
+    static int record(sli_model* m) {
+        hipStream_t s = m->stream;
+        SLI_TRY(embedding_launch(0, &m->st->token, m->emb, m->c.w_dtype, m->emb_s, m->x, m->V, m->D, s));
+        const long long ps = m->hd, hs = (long long)m->T * m->hd, ls = (long long)m->hkv * m->T * m->hd;
+        for (int l = 0; l < m->L; ++l) {
+            SLI_TRY(gemv_qkv(m, l));
+            SLI_TRY(mha_launch<KT>(m->q, (const KT*)m->kc, (const KT*)m->vc, m->attn, l, 0, &m->st->pos, m->T, m->hd,
+                                   m->hq, m->hkv, ps, hs, ls, m->part, s));
+            SLI_TRY(gemv_wo(m, l));
+            SLI_TRY(allreduce_x(m));
+            SLI_TRY(gemv_gu(m, l));
+            SLI_TRY(gemv_down(m, l));
+            SLI_TRY(allreduce_x(m));
+        }
+        SLI_TRY(gemv_lm(m));
+        hipLaunchKernelGGL(keyreduce_kernel, dim3(1), dim3(256), 0, s, m->keys, lm_head_blocks(m), m->st);
+        SLI_HIP(hipGetLastError());
+        if (m->c.tp_size > 1)
+            SLI_NCCL(ncclAllReduce(&m->st->key, &m->st->key, 1, ncclUint64, ncclMax, m->comm, s));
+        hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1), 0, s, m->st, m->prompt, m->hist, m->T);
+        SLI_HIP(hipGetLastError());
+        return SLI_OK;
+    }
+    // All weight-streaming launches of one step (for the roofline probe).
+    static int gemvs(sli_model* m) {
+        for (int l = 0; l < m->L; ++l) {
+            SLI_TRY(gemv_qkv(m, l));
+            SLI_TRY(gemv_wo(m, l));
+            SLI_TRY(gemv_gu(m, l));
+            SLI_TRY(gemv_down(m, l));
+        }
+        return gemv_lm(m);
+    }
+    static int fill_kv(sli_model* m, uint32_t seed, int upto) {
+        const uint64_t n = (uint64_t)m->L * m->hkv * upto * m->hd;
+        const int blocks = (int)std::min<uint64_t>(4096, (n + 255) / 256);
+        hipLaunchKernelGGL(fill_kv_kernel<KT>, dim3(blocks), dim3(256), 0, m->stream, (KT*)m->kc, (KT*)m->vc, m->L,
+                           m->hkv, m->T, m->hd, upto, m->c.n_kv_heads * m->hd, m->c.tp_rank * m->hkv, seed,
+                           SLI_SYNTH_C(1.0));
+        SLI_HIP(hipGetLastError());
+        return SLI_OK;
+    }
+    static int get_kv(sli_model* m, int layer, int which, int upto, float* tmp) {
+        const KT* base = (const KT*)(which == 0 ? m->kc : m->vc) + (size_t)layer * m->hkv * m->T * m->hd;
+        hipLaunchKernelGGL(get_kv_kernel<KT>, dim3(256), dim3(256), 0, m->stream, base, tmp, m->hkv, m->T, m->hd, upto);
+        SLI_HIP(hipGetLastError());
+        return SLI_OK;
+    }
+};
+
+#define SLI_DISPATCH(m, FN, ...)                                                                        \
+    ([&]() -> int {                                                                                     \
+        const int wd = (m)->c.w_dtype, kd = (m)->c.kv_dtype;                                            \
+        if (wd == SLI_DT_F16 && kd == SLI_DT_F16) return StepRecorder<__half, __half>::FN(__VA_ARGS__); \
+        if (wd == SLI_DT_F16 && kd == SLI_DT_F32) return StepRecorder<__half, float>::FN(__VA_ARGS__);  \
+        if (wd == SLI_DT_F32 && kd == SLI_DT_F16) return StepRecorder<float, __half>::FN(__VA_ARGS__);  \
+        if (wd == SLI_DT_F32 && kd == SLI_DT_F32) return StepRecorder<float, float>::FN(__VA_ARGS__);   \
+        if (wd == SLI_DT_I8 && kd == SLI_DT_F16) return StepRecorder<int8_t, __half>::FN(__VA_ARGS__);  \
+        return StepRecorder<int8_t, float>::FN(__VA_ARGS__);                                            \
+    })()
+
+static int capture(sli_model* m) {
+    if (m->graph_exec) return SLI_OK;
+    SLI_HIP(hipStreamBeginCapture(m->stream, hipStreamCaptureModeRelaxed));
+    int rc = SLI_DISPATCH(m, record, m);
+    hipGraph_t g = nullptr;
+    hipError_t e = hipStreamEndCapture(m->stream, &g);
+    if (rc != SLI_OK) {
+        if (g) (void)hipGraphDestroy(g);
+        return rc;
+    }
+    if (e != hipSuccess) return hip_fail(e, "hipStreamEndCapture");
+    m->graph = g;
+    SLI_HIP(hipGraphInstantiate(&m->graph_exec, g, nullptr, nullptr, 0));
+    return SLI_OK;
+}
+
+static int upload_state(sli_model* m, const DevState& h) {
+    SLI_HIP(hipMemcpyAsync(m->st, &h, sizeof(DevState), hipMemcpyHostToDevice, m->stream));
+    SLI_HIP(hipStreamSynchronize(m->stream));
+    return SLI_OK;
+}
+
+static int download_state(sli_model* m, DevState* h) {
+    SLI_HIP(hipMemcpyAsync(h, m->st, sizeof(DevState), hipMemcpyDeviceToHost, m->stream));
+    SLI_HIP(hipStreamSynchronize(m->stream));
+    return SLI_OK;
+}
+
+static void destroy(sli_model* m) {
+    if (!m) return;
+    (void)hipSetDevice(m->c.device);
+    if (m->stream) (void)hipStreamSynchronize(m->stream);
+    if (m->graph_exec) (void)hipGraphExecDestroy(m->graph_exec);
+    if (m->graph) (void)hipGraphDestroy(m->graph);
+    if (m->comm) ncclCommDestroy(m->comm);
+    for (void* p : m->allocs) (void)hipFree(p);
+    if (m->stream) (void)hipStreamDestroy(m->stream);
+    delete m;
+}
+
+}  // namespace sli
+
+using namespace sli;
+
+extern "C" {
+
+int sli_comm_id_bytes(void) { return (int)sizeof(ncclUniqueId); }
+
+int sli_comm_get_id(void* out) {
+    SLI_CHECK(out, SLI_ERR_ARG, "sli_comm_get_id: null");
+    ncclUniqueId id;
+    SLI_NCCL(ncclGetUniqueId(&id));
+    std::memcpy(out, &id, sizeof(id));
+    return SLI_OK;
+}
+
+int sli_model_create(const sli_model_config* cfg, const void* comm_id, sli_model** out) {
+    SLI_CHECK(cfg && out, SLI_ERR_ARG, "sli_model_create: null");
+    const sli_model_config& c = *cfg;
+    SLI_CHECK(c.vocab > 0 && c.dim > 0 && c.n_heads > 0 && c.n_kv_heads > 0 && c.head_dim > 0 && c.ffn > 0 &&
+                  c.n_layers > 0 && c.max_len > 0,
+              SLI_ERR_SHAPE, "sli_model_create: non-positive dimension");
+    SLI_CHECK(c.head_dim == 64 || c.head_dim == 128, SLI_ERR_SHAPE, "head_dim must be 64 or 128");
+    SLI_CHECK(c.n_heads * c.head_dim == c.dim, SLI_ERR_SHAPE, "n_heads * head_dim must equal dim");
+    SLI_CHECK(c.n_heads % c.n_kv_heads == 0, SLI_ERR_SHAPE, "n_heads must be a multiple of n_kv_heads");
+    const int g = c.n_heads / c.n_kv_heads;
+    SLI_CHECK(g == 1 || g == 2 || g == 4 || g == 8, SLI_ERR_SHAPE, "heads per kv head must be 1, 2, 4 or 8");
+    SLI_CHECK(c.tp_size >= 1 && c.tp_rank >= 0 && c.tp_rank < c.tp_size, SLI_ERR_ARG, "bad tp rank/size");
+    SLI_CHECK(c.n_kv_heads % c.tp_size == 0 && c.ffn % c.tp_size == 0, SLI_ERR_SHAPE,
+              "kv heads and ffn must divide by tp_size");
+    SLI_CHECK((c.ffn / c.tp_size) % 2 == 0, SLI_ERR_SHAPE, "local ffn must be even");
+    SLI_CHECK(c.w_dtype >= SLI_DT_F32 && c.w_dtype <= SLI_DT_I8, SLI_ERR_ARG, "bad w_dtype");
+    SLI_CHECK(c.kv_dtype == SLI_DT_F32 || c.kv_dtype == SLI_DT_F16, SLI_ERR_ARG, "bad kv_dtype");
+    SLI_CHECK(c.tp_size == 1 || comm_id, SLI_ERR_ARG, "tensor parallel needs a comm id");
+    const size_t wb = c.w_dtype == SLI_DT_F32 ? 4 : c.w_dtype == SLI_DT_F16 ? 2 : 1;
+    SLI_CHECK(((size_t)c.dim * wb) % 16 == 0 && ((size_t)(c.ffn / c.tp_size) * wb) % 16 == 0 &&
+                  ((size_t)(c.dim / c.tp_size) * wb) % 16 == 0,
+              SLI_ERR_SHAPE, "row bytes must be multiples of 16");
+    SLI_CHECK(c.dim <= kGemvMaxCols && c.ffn / c.tp_size <= kGemvMaxCols, SLI_ERR_SHAPE, "row too long for LDS staging");
+
+    SLI_HIP(hipSetDevice(c.device));
+    sli_model* m = new sli_model();
+    m->c = c;
+    auto bail = [&](int rc) {
+        destroy(m);
+        return rc;
+    };
+    if (hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess)
+        return bail(fail(SLI_ERR_HIP, "hipStreamCreate"));
+    m->D = c.dim;
+    m->L = c.n_layers;
+    m->T = c.max_len;
+    m->V = c.vocab;
+    m->hd = c.head_dim;
+    m->hq = c.n_heads / c.tp_size;
+    m->hkv = c.n_kv_heads / c.tp_size;
+    m->Il = c.ffn / c.tp_size;
+    const int vchunk = (c.vocab + c.tp_size - 1) / c.tp_size;
+    m->v_lo = c.tp_rank * vchunk;
+    m->v_n = std::max(0, std::min(vchunk, c.vocab - m->v_lo));
+    if (m->v_n <= 0) return bail(fail(SLI_ERR_SHAPE, "vocab shard is empty"));
+    m->wbytes = wb;
+    m->kvbytes = c.kv_dtype == SLI_DT_F32 ? 4 : 2;
+    const bool i8 = c.w_dtype == SLI_DT_I8;
+    const int D = m->D, hd = m->hd, qkv_rows = (m->hq + 2 * m->hkv) * hd;
+
+    int rc = SLI_OK;
+    auto A = [&](void** p, size_t bytes) {
+        if (rc == SLI_OK) rc = model_alloc(m, p, bytes);
+    };
+    A(&m->emb, (size_t)m->V * D * wb);
+    if (i8) A((void**)&m->emb_s, sizeof(float) * m->V);
+    A((void**)&m->norms, sizeof(float) * (size_t)(2 * m->L + 1) * D);
+    m->layers.resize(m->L);
+    for (auto& w : m->layers) {
+        A(&w.qkv, (size_t)qkv_rows * D * wb);
+        A(&w.wo, (size_t)D * m->hq * hd * wb);
+        A(&w.gu, (size_t)2 * m->Il * D * wb);
+        A(&w.down, (size_t)D * m->Il * wb);
+        if (i8) {
+            A((void**)&w.qkv_s, sizeof(float) * qkv_rows);
+            A((void**)&w.wo_s, sizeof(float) * D);
+            A((void**)&w.gu_s, sizeof(float) * 2 * m->Il);
+            A((void**)&w.down_s, sizeof(float) * D);
+        }
+    }
+    const size_t kv_elems = (size_t)m->L * m->hkv * m->T * hd;
+    A(&m->kc, kv_elems * m->kvbytes);
+    A(&m->vc, kv_elems * m->kvbytes);
+    A((void**)&m->x, sizeof(float) * D);
+    A((void**)&m->xpart, sizeof(float) * D);
+    A((void**)&m->q, sizeof(float) * m->hq * hd);
+    A((void**)&m->attn, sizeof(float) * m->hq * hd);
+    A((void**)&m->act, sizeof(float) * m->Il);
+    A((void**)&m->logits, sizeof(float) * m->v_n);
+    A((void**)&m->part, mha_workspace_bytes(m->T, m->hq, hd));
+    A((void**)&m->sin_t, sizeof(float) * (size_t)m->T * (hd / 2));
+    A((void**)&m->cos_t, sizeof(float) * (size_t)m->T * (hd / 2));
+    A((void**)&m->keys, sizeof(unsigned long long) * kGemvMaxBlocks);
+    A((void**)&m->st, sizeof(DevState));
+    A((void**)&m->prompt, sizeof(int32_t) * (m->T + 1));
+    A((void**)&m->hist, sizeof(int32_t) * (m->T + 1));
+    if (rc != SLI_OK) return bail(rc);
+
+    std::vector<float> s, co;
+    rope_table_host(hd, m->T, c.theta, s, co);  // rope_kernel.cpp:4-19, model.cpp:309-316
+    if (hipMemcpy(m->sin_t, s.data(), s.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(m->cos_t, co.data(), co.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+        return bail(fail(SLI_ERR_HIP, "rope table upload"));
+    if (hipMemset(m->prompt, 0, sizeof(int32_t) * (m->T + 1)) != hipSuccess ||
+        hipMemset(m->hist, 0, sizeof(int32_t) * (m->T + 1)) != hipSuccess)
+        return bail(fail(SLI_ERR_HIP, "memset"));
+    if ((rc = sli_model_reset(m)) != SLI_OK) return bail(rc);
+
+    if (c.tp_size > 1) {
+        ncclUniqueId id;
+        std::memcpy(&id, comm_id, sizeof(id));
+        ncclResult_t r = ncclCommInitRank(&m->comm, c.tp_size, id, c.tp_rank);
+        if (r != ncclSuccess) return bail(fail(SLI_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r)));
+    }
+    *out = m;
+    return SLI_OK;
+}
+
+int sli_model_destroy(sli_model* m) {
+    destroy(m);
+    return SLI_OK;
+}
+
+int sli_model_init_synthetic(sli_model* m, uint32_t seed) {
+    SLI_CHECK(m, SLI_ERR_ARG, "null model");
+    SLI_HIP(hipSetDevice(m->c.device));
+    auto src = [&](int kind, int index) {
+        return SrcSynth{seed, sli_stream_id((uint32_t)kind, (uint32_t)index), synth_c(m, kind),
+                        kind == SLI_T_NORM ? 1.0f : 0.0f};
+    };
+    SLI_TRY(place_tensor(m, SLI_T_EMB, 0, src(SLI_T_EMB, 0)));
+    for (int i = 0; i < 2 * m->L + 1; ++i) SLI_TRY(place_tensor(m, SLI_T_NORM, i, src(SLI_T_NORM, i)));
+    const int kinds[] = {SLI_T_WQ, SLI_T_WK, SLI_T_WV, SLI_T_WO, SLI_T_UP, SLI_T_GATE, SLI_T_DOWN};
+    for (int l = 0; l < m->L; ++l)
+        for (int k : kinds) SLI_TRY(place_tensor(m, k, l, src(k, l)));
+    SLI_HIP(hipStreamSynchronize(m->stream));
+    return SLI_OK;
+}
+
+int sli_model_set_weight(sli_model* m, int32_t kind, int32_t index, const float* host, int64_t n) {
+    SLI_CHECK(m && host, SLI_ERR_ARG, "null argument");
+    const int64_t want = tensor_elems(m, kind);
+    SLI_CHECK(want > 0, SLI_ERR_ARG, "unknown tensor kind");
+    SLI_CHECK(n == want, SLI_ERR_SHAPE, "tensor element count does not match the config");
+    SLI_HIP(hipSetDevice(m->c.device));
+    float* tmp = nullptr;
+    SLI_HIP(hipMalloc(&tmp, sizeof(float) * (size_t)n));
+    int rc = SLI_OK;
+    if (hipMemcpy(tmp, host, sizeof(float) * (size_t)n, hipMemcpyHostToDevice) != hipSuccess)
+        rc = fail(SLI_ERR_HIP, "hipMemcpy weight");
+    if (rc == SLI_OK) rc = place_tensor(m, kind, index, SrcBuf{tmp});
+    if (hipStreamSynchronize(m->stream) != hipSuccess && rc == SLI_OK) rc = fail(SLI_ERR_HIP, "sync");
+    (void)hipFree(tmp);
+    return rc;
+}
+
+int sli_model_load_flat(sli_model* m, const char* path) {
+    SLI_CHECK(m && path, SLI_ERR_ARG, "null argument");
+    const int fd = open(path, O_RDONLY);
+    SLI_CHECK(fd >= 0, SLI_ERR_ARG, std::string("Fail to open the weight file: ") + path);
+    struct stat sb;
+    if (fstat(fd, &sb) != 0) {
+        close(fd);
+        return fail(SLI_ERR_ARG, "fstat failed");
+    }
+    const int L = m->L;
+    int64_t total = tensor_elems(m, SLI_T_EMB) + (int64_t)(2 * L + 1) * m->D;
+    const int kinds[] = {SLI_T_WQ, SLI_T_WK, SLI_T_WV, SLI_T_WO, SLI_T_UP, SLI_T_GATE, SLI_T_DOWN};
+    for (int k : kinds) total += (int64_t)L * tensor_elems(m, k);
+    if ((int64_t)sb.st_size < total * 4) {
+        close(fd);
+        return fail(SLI_ERR_SHAPE, "weight file smaller than the config requires");
+    }
+    void* map = mmap(nullptr, (size_t)sb.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
+    close(fd);
+    if (map == MAP_FAILED) return fail(SLI_ERR_ARG, "mmap failed");  // (the reference tests !ptr, model.cpp:242)
+    const float* p = (const float*)map;
+    int rc = sli_model_set_weight(m, SLI_T_EMB, 0, p, tensor_elems(m, SLI_T_EMB));  // model.cpp:343-358
+    p += tensor_elems(m, SLI_T_EMB);
+    for (int i = 0; rc == SLI_OK && i < 2 * L + 1; ++i, p += m->D)  // :360-364
+        rc = sli_model_set_weight(m, SLI_T_NORM, i, p, m->D);
+    for (int k : kinds) {  // :366-468
+        const int64_t n = tensor_elems(m, k);
+        for (int l = 0; rc == SLI_OK && l < L; ++l, p += n) rc = sli_model_set_weight(m, k, l, p, n);
+    }
+    munmap(map, (size_t)sb.st_size);
+    return rc;
+}
+
+int sli_model_reset(sli_model* m) {
+    SLI_CHECK(m, SLI_ERR_ARG, "null model");
+    SLI_HIP(hipSetDevice(m->c.device));
+    const size_t kv = (size_t)m->L * m->hkv * m->T * m->hd * m->kvbytes;
+    SLI_HIP(hipMemsetAsync(m->kc, 0, kv, m->stream));
+    SLI_HIP(hipMemsetAsync(m->vc, 0, kv, m->stream));
+    DevState h{};
+    h.advance = 1;
+    return upload_state(m, h);
+}
+
+int sli_model_fill_kv_synthetic(sli_model* m, uint32_t seed, int32_t upto) {
+    SLI_CHECK(m, SLI_ERR_ARG, "null model");
+    SLI_CHECK(upto >= 0 && upto <= m->T, SLI_ERR_RANGE, "upto out of range");
+    if (upto == 0) return SLI_OK;
+    SLI_HIP(hipSetDevice(m->c.device));
+    SLI_TRY(SLI_DISPATCH(m, fill_kv, m, seed, upto));
+    SLI_HIP(hipStreamSynchronize(m->stream));
+    return SLI_OK;
+}
+
+int sli_model_set_state(sli_model* m, int32_t token, int32_t pos, int32_t advance) {
+    SLI_CHECK(m, SLI_ERR_ARG, "null model");
+    SLI_CHECK(token >= 0 && token < m->V, SLI_ERR_RANGE, "Token index is greater than vocab size.");
+    SLI_CHECK(pos >= 0 && pos < m->T, SLI_ERR_RANGE, "position out of range");
+    DevState h{};
+    SLI_TRY(download_state(m, &h));
+    h.token = token;
+    h.pos = pos;
+    h.advance = advance ? 1 : 0;
+    h.key = 0;
+    h.error = 0;
+    SLI_HIP(hipMemcpyAsync(m->hist + pos, &token, sizeof(int32_t), hipMemcpyHostToDevice, m->stream));
+    return upload_state(m, h);
+}
+
+int sli_model_set_prompt(sli_model* m, const int32_t* ids, int32_t n) {
+    SLI_CHECK(m && ids, SLI_ERR_ARG, "null argument");
+    SLI_CHECK(n >= 1 && n <= m->T, SLI_ERR_RANGE, "prompt length out of range");
+    for (int i = 0; i < n; ++i)
+        SLI_CHECK(ids[i] >= 0 && ids[i] < m->V, SLI_ERR_RANGE, "Token index is greater than vocab size.");
+    SLI_HIP(hipMemcpyAsync(m->prompt, ids, sizeof(int32_t) * n, hipMemcpyHostToDevice, m->stream));
+    DevState h{};
+    SLI_TRY(download_state(m, &h));
+    h.n_forced = n;
+    return upload_state(m, h);
+}
+
+int sli_model_get_state(sli_model* m, int32_t* pos, int32_t* token, int32_t* last_argmax, int32_t* error) {
+    SLI_CHECK(m, SLI_ERR_ARG, "null model");
+    DevState h{};
+    SLI_TRY(download_state(m, &h));
+    if (pos) *pos = h.pos;
+    if (token) *token = h.token;
+    if (last_argmax) *last_argmax = h.last_argmax;
+    if (error) *error = h.error;
+    return SLI_OK;
+}
+
+int sli_model_step(sli_model* m) {
+    SLI_CHECK(m, SLI_ERR_ARG, "null model");
+    SLI_TRY(capture(m));
+    SLI_HIP(hipGraphLaunch(m->graph_exec, m->stream));
+    return SLI_OK;
+}
+
+int sli_model_sync(sli_model* m) {
+    SLI_CHECK(m, SLI_ERR_ARG, "null model");
+    SLI_HIP(hipStreamSynchronize(m->stream));
+    return SLI_OK;
+}
+
+int sli_model_get_logits(sli_model* m, float* host, int32_t n, int32_t* vocab_lo) {
+    SLI_CHECK(m && host, SLI_ERR_ARG, "null argument");
+    SLI_CHECK(n >= m->v_n, SLI_ERR_SHAPE, "host buffer smaller than the local vocab shard");
+    SLI_HIP(hipMemcpyAsync(host, m->logits, sizeof(float) * m->v_n, hipMemcpyDeviceToHost, m->stream));
+    SLI_HIP(hipStreamSynchronize(m->stream));
+    if (vocab_lo) *vocab_lo = m->v_lo;
+    return SLI_OK;
+}
+
+int sli_model_predict(sli_model* m, const int32_t* prompt, int32_t n_prompt, int32_t max_length, int32_t* tokens_out,
+                      float* logits_out) {
+    SLI_CHECK(m && prompt && tokens_out, SLI_ERR_ARG, "null argument");
+    SLI_CHECK(max_length >= 1 && max_length <= m->T, SLI_ERR_RANGE, "max_length must be in [1, max_len]");
+    SLI_TRY(sli_model_set_prompt(m, prompt, n_prompt));
+    SLI_TRY(sli_model_set_state(m, prompt[0], 0, 1));
+    for (int t = 0; t < max_length; ++t) {  // model.cpp:157
+        SLI_TRY(sli_model_step(m));
+        if (logits_out) SLI_TRY(sli_model_get_logits(m, logits_out + (size_t)t * m->v_n, m->v_n, nullptr));
+    }
+    SLI_HIP(hipMemcpyAsync(tokens_out, m->hist, sizeof(int32_t) * max_length, hipMemcpyDeviceToHost, m->stream));
+    SLI_HIP(hipStreamSynchronize(m->stream));
+    return SLI_OK;
+}
+
+int sli_model_get_kv(sli_model* m, int32_t layer, int32_t which, int32_t upto, float* host) {
+    SLI_CHECK(m && host, SLI_ERR_ARG, "null argument");
+    SLI_CHECK(layer >= 0 && layer < m->L && upto > 0 && upto <= m->T && (which == 0 || which == 1), SLI_ERR_RANGE,
+              "layer/which/upto out of range");
+    const size_t n = (size_t)upto * m->hkv * m->hd;
+    float* tmp = nullptr;
+    SLI_HIP(hipMalloc(&tmp, n * 4));
+    int rc = SLI_DISPATCH(m, get_kv, m, layer, which, upto, tmp);
+    if (rc == SLI_OK && hipMemcpyAsync(host, tmp, n * 4, hipMemcpyDeviceToHost, m->stream) != hipSuccess)
+        rc = fail(SLI_ERR_HIP, "copy kv");
+    if (hipStreamSynchronize(m->stream) != hipSuccess && rc == SLI_OK) rc = fail(SLI_ERR_HIP, "sync");
+    (void)hipFree(tmp);
+    return rc;
+}
+
+int sli_model_stream(sli_model* m, sli_stream_t* out) {
+    SLI_CHECK(m && out, SLI_ERR_ARG, "null argument");
+    *out = m->stream;
+    return SLI_OK;
+}
+
+int sli_model_step_bytes(sli_model* m, double* weight_bytes, double* kv_bytes) {
+    SLI_CHECK(m, SLI_ERR_ARG, "null model");
+    DevState h{};
+    SLI_TRY(download_state(m, &h));
+    const double wb = (double)m->wbytes, D = m->D, hd = m->hd;
+    const double per_layer = ((m->hq + 2.0 * m->hkv) * hd * D + D * m->hq * hd + 3.0 * m->Il * D) * wb;
+    double w = m->L * per_layer + (double)m->v_n * D * wb;
+    if (m->c.w_dtype == SLI_DT_I8) w += 4.0 * (m->L * ((m->hq + 2.0 * m->hkv) * hd + 2.0 * D + 2.0 * m->Il) + m->v_n);
+    if (weight_bytes) *weight_bytes = w;
+    if (kv_bytes) *kv_bytes = 2.0 * m->L * (h.pos + 1.0) * m->hkv * hd * (double)m->kvbytes;
+    return SLI_OK;
+}
+
+int sli_model_time_gemv(sli_model* m, int32_t iters, double* avg_us, double* bytes_per_launch,
+                        int32_t* launches_per_step) {
+    SLI_CHECK(m && iters > 0, SLI_ERR_ARG, "bad argument");
+    SLI_HIP(hipSetDevice(m->c.device));
+    // the probe re-runs the step's GEMVs in place: save and restore the residual stream
+    float* xsave = nullptr;
+    SLI_HIP(hipMalloc(&xsave, sizeof(float) * m->D));
+    SLI_HIP(hipMemcpyAsync(xsave, m->x, sizeof(float) * m->D, hipMemcpyDeviceToDevice, m->stream));
+    hipEvent_t e0, e1;
+    SLI_HIP(hipEventCreate(&e0));
+    SLI_HIP(hipEventCreate(&e1));
+    int rc = SLI_DISPATCH(m, gemvs, m);  // warm-up
+    if (rc == SLI_OK) SLI_HIP(hipEventRecord(e0, m->stream));
+    for (int i = 0; rc == SLI_OK && i < iters; ++i) rc = SLI_DISPATCH(m, gemvs, m);
+    if (rc == SLI_OK) SLI_HIP(hipEventRecord(e1, m->stream));
+    SLI_HIP(hipEventSynchronize(e1));
+    float ms = 0.0f;
+    SLI_HIP(hipEventElapsedTime(&ms, e0, e1));
+    SLI_HIP(hipMemcpyAsync(m->x, xsave, sizeof(float) * m->D, hipMemcpyDeviceToDevice, m->stream));
+    SLI_HIP(hipStreamSynchronize(m->stream));
+    (void)hipFree(xsave);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (rc != SLI_OK) return rc;
+    const int n_launch = 4 * m->L + 1;
+    double wbytes = 0.0;
+    SLI_TRY(sli_model_step_bytes(m, &wbytes, nullptr));
+    if (avg_us) *avg_us = 1000.0 * ms / ((double)iters * n_launch);
+    if (bytes_per_launch) *bytes_per_launch = wbytes / n_launch;
+    if (launches_per_step) *launches_per_step = n_launch;
+    return SLI_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,191 @@
+"""``LlamaModel`` — Python mirror of the reference's model::LlamaModel (include/model/model.h:59-89)
+over the fused, graph-captured HIP decode step of libsli.so (engine.hip).
+
+Differences from the reference, all deliberate and documented in DESIGN.md:
+  * the model shape is a runtime ``LlamaModelConfig`` (the reference hard-codes config.h:5-17 and
+    copies it back in read_model_file, model.cpp:219-230);
+  * ``predict`` takes token ids (the sentencepiece tokenizer, encode.cpp:5-27, is out of scope);
+  * weights are either the reference's flat fp32 file (model_path) or seeded synthetic weights.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, replace
+
+import numpy as np
+
+from . import _lib
+from ._lib import DT_F16, DT_F32, DT_I8, ModelConfig, call
+
+_DTYPES = {"f32": DT_F32, "fp32": DT_F32, "f16": DT_F16, "fp16": DT_F16, "i8": DT_I8, "int8": DT_I8}
+
+
+@dataclass(frozen=True)
+class LlamaModelConfig:
+    """include/model/config.h:5-17 (same field names)."""
+    vocab_size: int = 128256
+    head_dim: int = 128
+    hidden_size: int = 3072
+    kv_hidden_size: int = 1024
+    intermediate_size: int = 8192
+    max_length: int = 1024
+    num_hidden_layers: int = 28
+    num_attention_heads: int = 24
+    num_key_value_heads: int = 8
+    rms_norm_eps: float = 1e-5
+    rope_theta: float = 100000.0
+
+
+PRESETS = {
+    # BASELINE.json configs[0]: tiny-llama shape (2 layers, d=256, 4 heads), greedy 32 tokens
+    "tiny": LlamaModelConfig(512, 64, 256, 256, 768, 64, 2, 4, 4, 1e-5, 10000.0),
+    "tiny-gqa": LlamaModelConfig(512, 64, 256, 128, 768, 64, 2, 4, 2, 1e-5, 10000.0),
+    # configs[1..3]: Llama-2 7B (public model card shape), ctx 2048
+    "llama2-7b": LlamaModelConfig(32000, 128, 4096, 4096, 11008, 2048, 32, 32, 32, 1e-5, 10000.0),
+    # configs[4]: Llama-3 8B (GQA), ctx 4096
+    "llama3-8b": LlamaModelConfig(128256, 128, 4096, 1024, 14336, 4096, 32, 32, 8, 1e-5, 500000.0),
+    # the reference's own hard-coded default (config.h:5-17, Llama-3.2-3B shape)
+    "reference-default": LlamaModelConfig(),
+}
+
+
+def preset(name: str, **overrides) -> LlamaModelConfig:
+    return replace(PRESETS[name], **overrides)
+
+
+class LlamaModel:
+    def __init__(self, tokenizer_path: str = "", model_path: str = "", device_type: str = "cuda",
+                 config: LlamaModelConfig | None = None, w_dtype: str = "f16", kv_dtype: str = "f16",
+                 act_mode: int = 0, tp_rank: int = 0, tp_size: int = 1, comm_id: bytes | None = None,
+                 device: int = 0, seed: int | None = None):
+        if device_type not in ("cuda", "hip"):
+            raise ValueError("Device Type ERROR!")  # op/*.cpp dispatch: only the HIP backend exists here
+        self.tokenizer_path = tokenizer_path
+        self.model_path = model_path
+        self.config = config or LlamaModelConfig()
+        self.w_dtype = _DTYPES[w_dtype]
+        self.kv_dtype = _DTYPES[kv_dtype]
+        self.act_mode = act_mode
+        self.tp_rank, self.tp_size = tp_rank, tp_size
+        self.comm_id = comm_id
+        self.device = device
+        self.seed = seed
+        self._h = None
+
+    # ------------------------------------------------------------------ model.h:63-67
+    def init(self) -> "LlamaModel":
+        c = self.config
+        if c.kv_hidden_size != c.num_key_value_heads * c.head_dim:
+            raise ValueError("kv_hidden_size must equal num_key_value_heads * head_dim")
+        mc = ModelConfig(c.vocab_size, c.hidden_size, c.num_attention_heads, c.num_key_value_heads, c.head_dim,
+                         c.intermediate_size, c.num_hidden_layers, c.max_length, c.rms_norm_eps, c.rope_theta,
+                         self.w_dtype, self.kv_dtype, self.act_mode, self.tp_rank, self.tp_size, self.device)
+        h = ctypes.c_void_p()
+        cid = ctypes.create_string_buffer(self.comm_id, len(self.comm_id)) if self.comm_id else None
+        call("sli_model_create", ctypes.byref(mc), cid, ctypes.byref(h))
+        self._h = h
+        if self.model_path:
+            call("sli_model_load_flat", self._h, self.model_path.encode())
+        elif self.seed is not None:
+            call("sli_model_init_synthetic", self._h, self.seed)
+        else:
+            raise ValueError("No model weigth file!")  # model.cpp:205-207
+        return self
+
+    def close(self):
+        if self._h is not None:
+            _lib.load().sli_model_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ weights / state
+    def set_weight(self, kind: int, index: int, tensor: np.ndarray):
+        t = np.ascontiguousarray(tensor, np.float32)
+        call("sli_model_set_weight", self._h, kind, index, t.ctypes.data_as(ctypes.c_void_p), t.size)
+
+    def reset(self):
+        call("sli_model_reset", self._h)
+
+    def fill_kv_synthetic(self, seed: int, upto: int):
+        call("sli_model_fill_kv_synthetic", self._h, seed, upto)
+
+    def set_state(self, token: int, pos: int, advance: bool = True):
+        call("sli_model_set_state", self._h, token, pos, 1 if advance else 0)
+
+    def set_prompt(self, ids):
+        a = np.ascontiguousarray(ids, np.int32)
+        call("sli_model_set_prompt", self._h, a.ctypes.data_as(ctypes.c_void_p), a.size)
+
+    def state(self):
+        p, t, a, e = (ctypes.c_int32() for _ in range(4))
+        call("sli_model_get_state", self._h, ctypes.byref(p), ctypes.byref(t), ctypes.byref(a), ctypes.byref(e))
+        return {"pos": p.value, "token": t.value, "last_argmax": a.value, "error": e.value}
+
+    @property
+    def local_vocab(self) -> int:
+        c = self.config
+        chunk = -(-c.vocab_size // self.tp_size)
+        return max(0, min(chunk, c.vocab_size - self.tp_rank * chunk))
+
+    # ------------------------------------------------------------------ model.cpp:40-140
+    def step(self):
+        call("sli_model_step", self._h)
+
+    def sync(self):
+        call("sli_model_sync", self._h)
+
+    def logits(self) -> tuple[np.ndarray, int]:
+        out = np.empty(self.local_vocab, np.float32)
+        lo = ctypes.c_int32()
+        call("sli_model_get_logits", self._h, out.ctypes.data_as(ctypes.c_void_p), out.size, ctypes.byref(lo))
+        return out, lo.value
+
+    def forward(self, token: int, pos: int) -> np.ndarray:
+        """One decode step at (token, pos); returns this rank's logits shard."""
+        self.set_state(token, pos, advance=False)
+        self.step()
+        return self.logits()[0]
+
+    # ------------------------------------------------------------------ model.cpp:142-187
+    def predict(self, prompt_ids, max_length: int, want_logits: bool = False):
+        p = np.ascontiguousarray(prompt_ids, np.int32)
+        toks = np.empty(max_length, np.int32)
+        logits = np.empty((max_length, self.local_vocab), np.float32) if want_logits else None
+        call("sli_model_predict", self._h, p.ctypes.data_as(ctypes.c_void_p), p.size, max_length,
+             toks.ctypes.data_as(ctypes.c_void_p), logits.ctypes.data_as(ctypes.c_void_p) if want_logits else None)
+        return (toks, logits) if want_logits else toks
+
+    def kv(self, layer: int, which: int, upto: int) -> np.ndarray:
+        c = self.config
+        out = np.empty((upto, c.num_key_value_heads // self.tp_size * c.head_dim), np.float32)
+        call("sli_model_get_kv", self._h, layer, which, upto, out.ctypes.data_as(ctypes.c_void_p))
+        return out
+
+    # ------------------------------------------------------------------ measurement
+    def stream(self) -> int:
+        s = ctypes.c_void_p()
+        call("sli_model_stream", self._h, ctypes.byref(s))
+        return s.value or 0
+
+    def step_bytes(self) -> tuple[float, float]:
+        w, k = ctypes.c_double(), ctypes.c_double()
+        call("sli_model_step_bytes", self._h, ctypes.byref(w), ctypes.byref(k))
+        return w.value, k.value
+
+    def time_gemv(self, iters: int = 20) -> dict:
+        us, b, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int32()
+        call("sli_model_time_gemv", self._h, iters, ctypes.byref(us), ctypes.byref(b), ctypes.byref(n))
+        return {"avg_us": us.value, "bytes_per_launch": b.value, "launches_per_step": n.value}
+
+
+def comm_id() -> bytes:
+    """A fresh RCCL unique id (rank 0 creates it and broadcasts it to the other ranks)."""
+    n = _lib.load().sli_comm_id_bytes()
+    buf = ctypes.create_string_buffer(n)
+    call("sli_comm_get_id", buf)
+    return buf.raw
