@@ -42,141 +42,163 @@ struct AttnGeom {
     static_assert(LPR >= 1 && LPR <= 64 && (64 % LPR) == 0, "head_dim / vector shape");
 };
 
+constexpr int kAttnWaves = 4;        // waves per workgroup = consecutive context slices of one kv head
+constexpr int kAttnMaxWgSplits = 128; // combine-kernel capacity (ctx <= 128 * 4 * PPW)
+
+// grid: n_kv_heads * wg_splits workgroups; wave w of workgroup (kvh, s) owns context slice 4s + w.
+// The 4 slice states are merged in LDS, so one partial per (q head, workgroup) reaches the workspace.
 template <typename KT, int HD, int G>
 __global__ void __launch_bounds__(256) attn_partial_kernel(AttnArgs<KT> a) {
     using Geo = AttnGeom<KT, HD>;
     constexpr int EPV = Geo::EPV, LPR = Geo::LPR, RPI = Geo::RPI, PPW = Geo::PPW;
+    __shared__ float sh[kAttnWaves][G][HD + 2];
     const int lane = threadIdx.x & 63;
-    const int wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    const int kvh = wid / a.max_splits;
-    const int split = wid - kvh * a.max_splits;
-    if (kvh >= a.n_kv_heads) return;
+    const int wave = threadIdx.x >> 6;
+    const int kvh = blockIdx.x / a.max_splits;  // max_splits counts workgroup splits here
+    const int wgs = blockIdx.x - kvh * a.max_splits;
     const int pos = a.pos_dev ? *a.pos_dev : a.pos_host;
-    const int t0 = split * PPW;
-    if (t0 > pos) return;  // slice beyond the live context: the combine never reads it
+    if (wgs * kAttnWaves * PPW > pos) return;  // whole workgroup past the live context (uniform exit)
+    const int t0 = (wgs * kAttnWaves + wave) * PPW;
+    const bool live_wave = t0 <= pos;
     const int t_end = min(t0 + PPW, pos + 1);
     const int sub = lane / LPR;
     const int li = lane - sub * LPR;
 
-    const KT* kb = a.k + (long long)kvh * a.head_stride + li * EPV;
-    const KT* vb = a.v + (long long)kvh * a.head_stride + li * EPV;
-    u32x4 kr[kAttnNit], vr[kAttnNit];
-#pragma unroll
-    for (int it = 0; it < kAttnNit; ++it) {
-        const int t = min(t0 + it * RPI + sub, t_end - 1);  // clamp, never branch around a load
-        kr[it] = load16<false>(kb + (long long)t * a.pos_stride);
-    }
-#pragma unroll
-    for (int it = 0; it < kAttnNit; ++it) {
-        const int t = min(t0 + it * RPI + sub, t_end - 1);
-        vr[it] = load16<false>(vb + (long long)t * a.pos_stride);
-    }
-
-    float qv[G][EPV];
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-        for (int e = 0; e < EPV; ++e) qv[g][e] = a.q[(size_t)(kvh * G + g) * HD + li * EPV + e];
-
-    float s[kAttnNit][G];
-    float m[G];
-#pragma unroll
-    for (int g = 0; g < G; ++g) m[g] = -INFINITY;
-#pragma unroll
-    for (int it = 0; it < kAttnNit; ++it) {
-        float kf[EPV];
-        Vec16<KT>::unpack(kr[it], kf);
-        const bool live = (t0 + it * RPI + sub) < t_end;
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            float d = 0.0f;
-#pragma unroll
-            for (int e = 0; e < EPV; ++e) d = fmaf(qv[g][e], kf[e], d);
-            d = group_sum<LPR>(d);
-            s[it][g] = live ? d * a.scale : -INFINITY;
-            m[g] = fmaxf(m[g], s[it][g]);
-        }
-    }
-    float l[G];
+    float m[G], l[G], ov[G][EPV];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-#pragma unroll
-        for (int o = LPR; o < 64; o <<= 1) m[g] = fmaxf(m[g], __shfl_xor(m[g], o, kWave));
+        m[g] = -INFINITY;
         l[g] = 0.0f;
-    }
-    float ov[G][EPV];
-#pragma unroll
-    for (int g = 0; g < G; ++g)
 #pragma unroll
         for (int e = 0; e < EPV; ++e) ov[g][e] = 0.0f;
+    }
+    if (live_wave) {
+        const KT* kb = a.k + (long long)kvh * a.head_stride + li * EPV;
+        const KT* vb = a.v + (long long)kvh * a.head_stride + li * EPV;
+        u32x4 kr[kAttnNit], vr[kAttnNit];
 #pragma unroll
-    for (int it = 0; it < kAttnNit; ++it) {
-        float vf[EPV];
-        Vec16<KT>::unpack(vr[it], vf);
+        for (int it = 0; it < kAttnNit; ++it) {
+            const int t = min(t0 + it * RPI + sub, t_end - 1);  // clamp, never branch around a load
+            kr[it] = load16<false>(kb + (long long)t * a.pos_stride);
+        }
+#pragma unroll
+        for (int it = 0; it < kAttnNit; ++it) {
+            const int t = min(t0 + it * RPI + sub, t_end - 1);
+            vr[it] = load16<false>(vb + (long long)t * a.pos_stride);
+        }
+        float qv[G][EPV];
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int e = 0; e < EPV; ++e) qv[g][e] = a.q[(size_t)(kvh * G + g) * HD + li * EPV + e];
+        float s[kAttnNit][G];
+#pragma unroll
+        for (int it = 0; it < kAttnNit; ++it) {
+            float kf[EPV];
+            Vec16<KT>::unpack(kr[it], kf);
+            const bool live = (t0 + it * RPI + sub) < t_end;
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                float d = 0.0f;
+#pragma unroll
+                for (int e = 0; e < EPV; ++e) d = fmaf(qv[g][e], kf[e], d);
+                d = group_sum<LPR>(d);
+                s[it][g] = live ? d * a.scale : -INFINITY;  // mha_kernel.cpp:51-60 (sum * scale)
+                m[g] = fmaxf(m[g], s[it][g]);
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int o = LPR; o < 64; o <<= 1) m[g] = fmaxf(m[g], __shfl_xor(m[g], o, kWave));
+#pragma unroll
+        for (int it = 0; it < kAttnNit; ++it) {
+            float vf[EPV];
+            Vec16<KT>::unpack(vr[it], vf);
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const float p = expf(s[it][g] - m[g]);  // 0 for masked rows
+                l[g] += p;
+#pragma unroll
+                for (int e = 0; e < EPV; ++e) ov[g][e] = fmaf(p, vf[e], ov[g][e]);
+            }
+        }
+        // every lane of a row group holds the same p: reduce across row groups only
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-            const float p = expf(s[it][g] - m[g]);  // 0 for masked rows
-            l[g] += p;
 #pragma unroll
-            for (int e = 0; e < EPV; ++e) ov[g][e] = fmaf(p, vf[e], ov[g][e]);
-        }
-    }
-    // l was accumulated once per lane of a row group (LPR copies of each row): reduce across row groups only
+            for (int o = LPR; o < 64; o <<= 1) {
+                l[g] += __shfl_xor(l[g], o, kWave);
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-#pragma unroll
-        for (int o = LPR; o < 64; o <<= 1) {
-            l[g] += __shfl_xor(l[g], o, kWave);
-#pragma unroll
-            for (int e = 0; e < EPV; ++e) ov[g][e] += __shfl_xor(ov[g][e], o, kWave);
+                for (int e = 0; e < EPV; ++e) ov[g][e] += __shfl_xor(ov[g][e], o, kWave);
+            }
         }
     }
     if (sub == 0) {
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-            float* dst = a.part + ((size_t)(kvh * G + g) * a.max_splits + split) * (HD + 2);
 #pragma unroll
-            for (int e = 0; e < EPV; ++e) dst[li * EPV + e] = ov[g][e];
+            for (int e = 0; e < EPV; ++e) sh[wave][g][li * EPV + e] = ov[g][e];
             if (li == 0) {
-                dst[HD] = m[g];
-                dst[HD + 1] = l[g];
+                sh[wave][g][HD] = m[g];
+                sh[wave][g][HD + 1] = l[g];
             }
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < G * HD; i += blockDim.x) {
+        const int g = i / HD, d = i - g * HD;
+        float M = -INFINITY;
+#pragma unroll
+        for (int w = 0; w < kAttnWaves; ++w) M = fmaxf(M, sh[w][g][HD]);
+        float o = 0.0f, L = 0.0f;
+#pragma unroll
+        for (int w = 0; w < kAttnWaves; ++w) {
+            const float c = expf(sh[w][g][HD] - M);  // dead waves: m = -inf -> 0
+            o = fmaf(c, sh[w][g][d], o);
+            L = fmaf(c, sh[w][g][HD + 1], L);
+        }
+        float* dst = a.part + ((size_t)(kvh * G + g) * a.max_splits + wgs) * (HD + 2);
+        dst[d] = o;
+        if (d == 0) {
+            dst[HD] = M;
+            dst[HD + 1] = L;
         }
     }
 }
 
-// One wave per query head: merge the live slices.
+// One workgroup per query head: merge the live workgroup partials (independent loads per split).
 template <int HD>
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(256)
     attn_combine_kernel(const float* __restrict__ part, float* __restrict__ out, const int32_t* pos_dev,
-                        int pos_host, int max_splits, int ppw) {
+                        int pos_host, int max_splits, int ppw_wg) {
+    __shared__ float sw[kAttnMaxWgSplits];
+    __shared__ float sL;
     const int h = blockIdx.x;
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x;
     const int pos = pos_dev ? *pos_dev : pos_host;
-    const int ns = pos / ppw + 1;
+    const int ns = pos / ppw_wg + 1;
     const float* ph = part + (size_t)h * max_splits * (HD + 2);
-    float mx = -INFINITY;
-    for (int i = lane; i < ns; i += 64) mx = fmaxf(mx, ph[(size_t)i * (HD + 2) + HD]);
-    mx = wave_max(mx);
-    constexpr int DPL = (HD + 63) / 64;
-    float o[DPL];
-#pragma unroll
-    for (int j = 0; j < DPL; ++j) o[j] = 0.0f;
-    float L = 0.0f;
-    for (int i = 0; i < ns; ++i) {
-        const float* pi = ph + (size_t)i * (HD + 2);
-        const float w = expf(pi[HD] - mx);
-        L = fmaf(w, pi[HD + 1], L);
-#pragma unroll
-        for (int j = 0; j < DPL; ++j) {
-            const int d = lane + 64 * j;
-            if (d < HD) o[j] = fmaf(w, pi[d], o[j]);
+    if (tid < 64) {
+        float mx = -INFINITY;
+        for (int i = tid; i < ns; i += 64) mx = fmaxf(mx, ph[(size_t)i * (HD + 2) + HD]);
+        mx = wave_max(mx);
+        float L = 0.0f;
+        for (int i = tid; i < ns; i += 64) {
+            const float w = expf(ph[(size_t)i * (HD + 2) + HD] - mx);
+            sw[i] = w;
+            L = fmaf(w, ph[(size_t)i * (HD + 2) + HD + 1], L);
         }
+        L = wave_sum(L);
+        if (tid == 0) sL = L;
     }
-#pragma unroll
-    for (int j = 0; j < DPL; ++j) {
-        const int d = lane + 64 * j;
-        if (d < HD) out[(size_t)h * HD + d] = o[j] / L;
+    __syncthreads();
+    const float L = sL;
+    for (int d = tid; d < HD; d += blockDim.x) {
+        float o = 0.0f;
+#pragma unroll 8
+        for (int i = 0; i < ns; ++i) o = fmaf(sw[i], ph[(size_t)i * (HD + 2) + d], o);
+        out[(size_t)h * HD + d] = o / L;
     }
 }
 

@@ -303,7 +303,7 @@ struct StepRecorder {
         KT* kc = (KT*)m->kc + (size_t)l * m->hkv * m->T * m->hd;
         KT* vc = (KT*)m->vc + (size_t)l * m->hkv * m->T * m->hd;
         EpiQKV<KT> e{m->q, kc, vc, w.qkv_s, &m->st->pos, m->sin_t, m->cos_t, m->hq, m->hkv, m->hd, m->T};
-        SLI_HIP((launch_gemv<WT, 4, 4, NT>((const WT*)w.qkv, in, e, (m->hq + 2 * m->hkv) * (m->hd / 4), m->stream)));
+        SLI_HIP((launch_gemv<WT, 2, 8, NT>((const WT*)w.qkv, in, e, (m->hq + 2 * m->hkv) * (m->hd / 2), m->stream)));
         return SLI_OK;
     }
     static int gemv_wo(sli_model* m, int l) {
@@ -318,7 +318,7 @@ struct StepRecorder {
         const LayerW& w = m->layers[l];
         GemvIn in{m->x, m->norms + (size_t)(2 * l + 1) * m->D, m->c.eps, m->D};
         EpiSwiGLU e{m->act, w.gu_s, m->Il, m->c.act_mode};
-        SLI_HIP((launch_gemv<WT, 4, 4, NT>((const WT*)w.gu, in, e, m->Il / 2, m->stream)));
+        SLI_HIP((launch_gemv<WT, 2, 8, NT>((const WT*)w.gu, in, e, m->Il, m->stream)));
         return SLI_OK;
     }
     static int gemv_down(sli_model* m, int l) {

@@ -22,27 +22,46 @@ struct GemvIn {
     int cols;
 };
 
-constexpr int kGemvThreads = 256;
+constexpr int kGemvThreads = 1024;  // one persistent 16-wave workgroup per CU: x staged once per CU
 constexpr int kGemvLdsHead = 64;  // floats of reduction scratch in front of the staged x
 
 inline size_t gemv_lds_bytes(int cols) { return sizeof(float) * (size_t)(kGemvLdsHead + cols); }
 
-// Stage x (optionally RMS-normalised) into LDS. All LDS lives in one dynamic array (G17: no static
-// __shared__ in front of the dynamic region, so the b128 reads stay 16-byte aligned).
+constexpr int kGemvStageV4 = 4;  // float4 of x per thread: 1024 threads x 4 x 4 = 16384 columns
+
+// Stage x (optionally RMS-normalised) into LDS in ONE round trip: every thread issues all of its float4
+// loads of x (and of the norm weight) before using any (clamped indices, no branch around a load).
+// All LDS lives in one dynamic array (G17: no static __shared__ in front of the dynamic region, so the
+// b128 reads stay 16-byte aligned). Requires cols % 4 == 0 and 16-byte aligned x / norm_w.
 __device__ __forceinline__ void gemv_stage_x(float* smem, const GemvIn& in) {
     float* red = smem;
     float* xs = smem + kGemvLdsHead;
     const int tid = threadIdx.x;
     const int nt = blockDim.x;
+    const int n4 = in.cols >> 2;
+    const float4* x4 = reinterpret_cast<const float4*>(in.x);
+    float4 xr[kGemvStageV4];
+#pragma unroll
+    for (int k = 0; k < kGemvStageV4; ++k) xr[k] = x4[min(tid + k * nt, n4 - 1)];
     if (in.norm_w == nullptr) {
-        for (int c = tid; c < in.cols; c += nt) xs[c] = in.x[c];
+#pragma unroll
+        for (int k = 0; k < kGemvStageV4; ++k)
+            if (tid + k * nt < n4) reinterpret_cast<float4*>(xs)[tid + k * nt] = xr[k];
         return;
     }
+    const float4* w4 = reinterpret_cast<const float4*>(in.norm_w);
+    float4 wr[kGemvStageV4];
+#pragma unroll
+    for (int k = 0; k < kGemvStageV4; ++k) wr[k] = w4[min(tid + k * nt, n4 - 1)];
     float ss = 0.0f;
-    for (int c = tid; c < in.cols; c += nt) {
-        float v = in.x[c];
-        xs[c] = v;
-        ss += v * v;
+#pragma unroll
+    for (int k = 0; k < kGemvStageV4; ++k) {
+        if (tid + k * nt < n4) {
+            ss += xr[k].x * xr[k].x;
+            ss += xr[k].y * xr[k].y;
+            ss += xr[k].z * xr[k].z;
+            ss += xr[k].w * xr[k].w;
+        }
     }
     ss = wave_sum(ss);
     const int wave = tid >> 6;
@@ -51,21 +70,59 @@ __device__ __forceinline__ void gemv_stage_x(float* smem, const GemvIn& in) {
     if (tid == 0) {
         float t = 0.0f;
         for (int w = 0; w < (nt >> 6); ++w) t += red[w];
-        float tep = t / (float)in.cols;   // rms_kernel.cpp:17
-        float rms = sqrtf(tep + in.eps);  // :18
-        red[32] = 1.0f / rms;             // :19
+        const float tep = t / (float)in.cols;  // rms_kernel.cpp:17
+        const float rms = sqrtf(tep + in.eps);  // :18
+        red[32] = 1.0f / rms;                   // :19
     }
     __syncthreads();
     const float inv = red[32];
-    for (int c = tid; c < in.cols; c += nt) xs[c] = (xs[c] * inv) * in.norm_w[c];  // :20-22
+#pragma unroll
+    for (int k = 0; k < kGemvStageV4; ++k) {
+        if (tid + k * nt < n4) {  // :20-22  y = (x * inv) * w
+            float4 o;
+            o.x = (xr[k].x * inv) * wr[k].x;
+            o.y = (xr[k].y * inv) * wr[k].y;
+            o.z = (xr[k].z * inv) * wr[k].z;
+            o.w = (xr[k].w * inv) * wr[k].w;
+            reinterpret_cast<float4*>(xs)[tid + k * nt] = o;
+        }
+    }
 }
 
+// acc[r] += sum over the U vectors (64 lanes apart, starting at vector index v) of W[r] . x
+template <typename WT, int R, int U>
+__device__ __forceinline__ void gemv_chunk(const u32x4 (&w)[U][R], const float* xs, int v, float* acc) {
+    constexpr int EPV = Vec16<WT>::N;
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        float xv[EPV];
+        const float4* xp = reinterpret_cast<const float4*>(xs + (size_t)(v + j * 64) * EPV);
+#pragma unroll
+        for (int e = 0; e < EPV / 4; ++e) {
+            float4 t = xp[e];
+            xv[4 * e] = t.x;
+            xv[4 * e + 1] = t.y;
+            xv[4 * e + 2] = t.z;
+            xv[4 * e + 3] = t.w;
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            float wf[EPV];
+            Vec16<WT>::unpack(w[j][r], wf);
+#pragma unroll
+            for (int e = 0; e < EPV; ++e) acc[r] = fmaf(wf[e], xv[e], acc[r]);
+        }
+    }
+}
+
+// Balanced static schedule: wave gw of W owns units [gw*N/W, (gw+1)*N/W) (sizes differ by at most one),
+// so no wave is left with a second pass while the rest of the chip idles. The first weight chunk of the
+// wave's first unit is issued BEFORE the x-staging prologue, so the prologue's L2 round trips and
+// barriers overlap the first HBM round trip instead of preceding it.
 template <typename WT, int R, int U, bool NT, class Epi>
 __global__ void __launch_bounds__(kGemvThreads) gemv_kernel(const WT* __restrict__ W, GemvIn in, Epi epi_in) {
     Epi epi = epi_in;  // mutable per-thread copy (EpiLogits keeps a running key)
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    gemv_stage_x(smem, in);
-    __syncthreads();
     const float* xs = smem + kGemvLdsHead;
 
     constexpr int EPV = Vec16<WT>::N;
@@ -76,70 +133,58 @@ __global__ void __launch_bounds__(kGemvThreads) gemv_kernel(const WT* __restrict
     const int nvec = cols / EPV;
     const size_t row_bytes = (size_t)cols * sizeof(WT);
     const int nunits = epi.units();
+    const long long gw = (long long)blockIdx.x * nwaves + wave;
+    const long long nw = (long long)gridDim.x * nwaves;
+    const int u_begin = (int)(gw * nunits / nw);
+    const int u_end = (int)((gw + 1) * nunits / nw);
 
-    for (int u = blockIdx.x * nwaves + wave; u < nunits; u += gridDim.x * nwaves) {
+    // prefetch: first U-chunk of the first unit (full chunk only when it lies inside the row)
+    const bool have_pre = u_begin < u_end && lane + (U - 1) * 64 < nvec;
+    u32x4 pre[U][R];
+    if (have_pre) {
+        int rows[R];
+        epi.rows(u_begin, rows);
+#pragma unroll
+        for (int j = 0; j < U; ++j)
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                pre[j][r] = load16<NT>(reinterpret_cast<const char*>(W) + (size_t)rows[r] * row_bytes +
+                                       (size_t)(lane + j * 64) * 16);
+    }
+    gemv_stage_x(smem, in);
+    __syncthreads();
+
+    float acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = 0.0f;
+    if (have_pre) gemv_chunk<WT, R, U>(pre, xs, lane, acc);  // peeled: pre dies here
+
+    for (int u = u_begin; u < u_end; ++u) {
         int rows[R];
         epi.rows(u, rows);
         const char* wp[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) wp[r] = reinterpret_cast<const char*>(W) + (size_t)rows[r] * row_bytes;
-        float acc[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) acc[r] = 0.0f;
-
-        int v = lane;
+        int v = (u == u_begin && have_pre) ? lane + U * 64 : lane;
         for (; v + (U - 1) * 64 < nvec; v += U * 64) {
             u32x4 w[U][R];
 #pragma unroll
             for (int j = 0; j < U; ++j)
 #pragma unroll
                 for (int r = 0; r < R; ++r) w[j][r] = load16<NT>(wp[r] + (size_t)(v + j * 64) * 16);
-#pragma unroll
-            for (int j = 0; j < U; ++j) {
-                float xv[EPV];
-                const float4* xp = reinterpret_cast<const float4*>(xs + (size_t)(v + j * 64) * EPV);
-#pragma unroll
-                for (int e = 0; e < EPV / 4; ++e) {
-                    float4 t = xp[e];
-                    xv[4 * e] = t.x;
-                    xv[4 * e + 1] = t.y;
-                    xv[4 * e + 2] = t.z;
-                    xv[4 * e + 3] = t.w;
-                }
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    float wf[EPV];
-                    Vec16<WT>::unpack(w[j][r], wf);
-#pragma unroll
-                    for (int e = 0; e < EPV; ++e) acc[r] = fmaf(wf[e], xv[e], acc[r]);
-                }
-            }
+            gemv_chunk<WT, R, U>(w, xs, v, acc);
         }
         for (; v < nvec; v += 64) {
-            u32x4 w[R];
+            u32x4 w[1][R];
 #pragma unroll
-            for (int r = 0; r < R; ++r) w[r] = load16<NT>(wp[r] + (size_t)v * 16);
-            float xv[EPV];
-            const float4* xp = reinterpret_cast<const float4*>(xs + (size_t)v * EPV);
-#pragma unroll
-            for (int e = 0; e < EPV / 4; ++e) {
-                float4 t = xp[e];
-                xv[4 * e] = t.x;
-                xv[4 * e + 1] = t.y;
-                xv[4 * e + 2] = t.z;
-                xv[4 * e + 3] = t.w;
-            }
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                float wf[EPV];
-                Vec16<WT>::unpack(w[r], wf);
-#pragma unroll
-                for (int e = 0; e < EPV; ++e) acc[r] = fmaf(wf[e], xv[e], acc[r]);
-            }
+            for (int r = 0; r < R; ++r) w[0][r] = load16<NT>(wp[r] + (size_t)v * 16);
+            gemv_chunk<WT, R, 1>(w, xs, v, acc);
         }
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r] = wave_sum(acc[r]);
         epi.store(u, rows, acc, lane);
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] = 0.0f;
     }
     epi.finish(smem);
 }
@@ -192,10 +237,10 @@ struct EpiStore {
     __device__ void finish(float*) const {}
 };
 
-// Fused q/k/v projection + RoPE + KV-cache write (model.cpp:54-67): rows of the fused [q; k; v] weight
-// are taken as RoPE pairs {d, d+1, d+hd/2, d+1+hd/2} of one head, so the rotation
-// (rope_kernel.cpp:31-38) happens on the row sums in registers and K/V go straight into the
-// head-major cache [kv_head][T][hd] of this layer.
+// Fused q/k/v projection + RoPE + KV-cache write (model.cpp:54-67): a unit is the RoPE pair of rows
+// {d, d+hd/2} of one head of the fused [q; k; v] weight, so the rotation (rope_kernel.cpp:31-38) is
+// applied to the two row sums in registers and K/V go straight into the head-major cache
+// [kv_head][T][hd] of this layer.
 template <typename KT>
 struct EpiQKV {
     float* q_out;              // [hq*hd]
@@ -206,90 +251,69 @@ struct EpiQKV {
     const float* sin_t;        // [T][hd/2]
     const float* cos_t;
     int hq, hkv, hd, T;
-    __device__ int units() const { return (hq + 2 * hkv) * (hd / 4); }
+    __device__ int units() const { return (hq + 2 * hkv) * (hd / 2); }
     __device__ void rows(int u, int* r) const {
-        const int per = hd / 4;
-        const int uh = u / per;
-        const int d = (u - uh * per) * 2;
-        const int base = uh * hd;
-        r[0] = base + d;
-        r[1] = base + d + 1;
-        r[2] = base + d + hd / 2;
-        r[3] = base + d + 1 + hd / 2;
+        const int half = hd / 2;
+        const int uh = u / half;
+        const int d = u - uh * half;
+        r[0] = uh * hd + d;
+        r[1] = uh * hd + d + half;
     }
     __device__ void store(int u, const int* r, const float* acc, int lane) const {
         if (lane != 0) return;
-        const int per = hd / 4;
-        const int uh = u / per;
-        const int d = (u - uh * per) * 2;
-        float a0 = acc[0], a1 = acc[1], a2 = acc[2], a3 = acc[3];
+        const int half = hd / 2;
+        const int uh = u / half;
+        const int d = u - uh * half;
+        float a0 = acc[0], a1 = acc[1];
         if (rscale) {
             a0 *= rscale[r[0]];
             a1 *= rscale[r[1]];
-            a2 *= rscale[r[2]];
-            a3 *= rscale[r[3]];
         }
         const int pos = *pos_dev;
         if (uh < hq + hkv) {  // q or k: rotate (rope_kernel.cpp:30-38)
-            const float s0 = sin_t[pos * (hd / 2) + d], c0 = cos_t[pos * (hd / 2) + d];
-            const float s1 = sin_t[pos * (hd / 2) + d + 1], c1 = cos_t[pos * (hd / 2) + d + 1];
-            const float r0 = a0 * c0 - a2 * s0, r2 = a2 * c0 + a0 * s0;
-            const float r1 = a1 * c1 - a3 * s1, r3 = a3 * c1 + a1 * s1;
+            const float fci = sin_t[pos * half + d], fcr = cos_t[pos * half + d];
+            const float r0 = a0 * fcr - a1 * fci;
+            const float r1 = a1 * fcr + a0 * fci;
             if (uh < hq) {
                 float* q = q_out + (size_t)uh * hd;
                 q[d] = r0;
-                q[d + 1] = r1;
-                q[d + hd / 2] = r2;
-                q[d + 1 + hd / 2] = r3;
+                q[d + half] = r1;
             } else {
                 KT* k = kc + ((size_t)(uh - hq) * T + pos) * hd;
                 k[d] = from_f32<KT>(r0);
-                k[d + 1] = from_f32<KT>(r1);
-                k[d + hd / 2] = from_f32<KT>(r2);
-                k[d + 1 + hd / 2] = from_f32<KT>(r3);
+                k[d + half] = from_f32<KT>(r1);
             }
         } else {
             KT* v = vc + ((size_t)(uh - hq - hkv) * T + pos) * hd;
             v[d] = from_f32<KT>(a0);
-            v[d + 1] = from_f32<KT>(a1);
-            v[d + hd / 2] = from_f32<KT>(a2);
-            v[d + 1 + hd / 2] = from_f32<KT>(a3);
+            v[d + half] = from_f32<KT>(a1);
         }
     }
     __device__ void finish(float*) const {}
 };
 
 // Fused gate/up projection + activation (model.cpp:99-115): fused weight rows [gate(I); up(I)], unit =
-// {gate i, gate i+1, up i, up i+1}; act = sigmoid(g)*u (swiglu_kernel.cpp:12-13) or SiLU(g)*u.
+// {gate i, up i}; act = sigmoid(g)*u (swiglu_kernel.cpp:12-13) or SiLU(g)*u.
 struct EpiSwiGLU {
     float* act;
     const float* rscale;
-    int inter;  // I (local), even
+    int inter;  // I (local)
     int silu;
-    __device__ int units() const { return inter / 2; }
+    __device__ int units() const { return inter; }
     __device__ void rows(int u, int* r) const {
-        r[0] = 2 * u;
-        r[1] = 2 * u + 1;
-        r[2] = inter + 2 * u;
-        r[3] = inter + 2 * u + 1;
+        r[0] = u;
+        r[1] = inter + u;
     }
     __device__ void store(int u, const int* r, const float* acc, int lane) const {
         if (lane != 0) return;
-        float g0 = acc[0], g1 = acc[1], u0 = acc[2], u1 = acc[3];
+        float g = acc[0], up = acc[1];
         if (rscale) {
-            g0 *= rscale[r[0]];
-            g1 *= rscale[r[1]];
-            u0 *= rscale[r[2]];
-            u1 *= rscale[r[3]];
+            g *= rscale[r[0]];
+            up *= rscale[r[1]];
         }
-        float t0 = 1.0f / (1.0f + expf(-g0));
-        float t1 = 1.0f / (1.0f + expf(-g1));
-        if (silu) {
-            t0 = g0 * t0;
-            t1 = g1 * t1;
-        }
-        act[2 * u] = t0 * u0;
-        act[2 * u + 1] = t1 * u1;
+        float t = 1.0f / (1.0f + expf(-g));
+        if (silu) t = g * t;
+        act[u] = t * up;
     }
     __device__ void finish(float*) const {}
 };
@@ -340,9 +364,12 @@ struct EpiLogits {
 
 namespace sli {
 
-constexpr int kGemvMaxCols = 16384 - kGemvLdsHead;  // x staged in <= 64 KiB of LDS
-constexpr int kGemvMaxBlocks = 1024;                 // 4 workgroups per CU, grid-stride beyond
+constexpr int kGemvMaxCols = 16384 - kGemvLdsHead;  // x staged in 64 KiB of LDS (<= kGemvThreads*4*kGemvStageV4)
+constexpr int kGemvCUs = 256;                                  // MI355X: 8 XCDs x 32 CUs
+constexpr int kGemvMaxBlocks = kGemvCUs;                       // persistent grid: one workgroup per CU
 
+// Grid: enough workgroups for every unit to have a wave, capped at the persistent size; the balanced
+// schedule in gemv_kernel spreads the units over whatever grid this returns.
 inline int gemv_blocks(int units) {
     int b = (units + (kGemvThreads / 64) - 1) / (kGemvThreads / 64);
     return b < kGemvMaxBlocks ? (b > 0 ? b : 1) : kGemvMaxBlocks;

@@ -138,7 +138,8 @@ __global__ void __launch_bounds__(1024) argmax_kernel(const float* __restrict__ 
 template <typename WT>
 static int matmul_dispatch(const float* x, const WT* w, const float* rscale, float* y, int rows, int cols, float scale,
                            hipStream_t s) {
-    const bool vec_ok = ((uintptr_t)w % 16 == 0) && (((size_t)cols * sizeof(WT)) % 16 == 0) && cols <= kGemvMaxCols;
+    const bool vec_ok = ((uintptr_t)w % 16 == 0) && ((uintptr_t)x % 16 == 0) && (cols % 4 == 0) &&
+                        (((size_t)cols * sizeof(WT)) % 16 == 0) && cols <= kGemvMaxCols;
     if (vec_ok) {
         EpiStore<2> epi{y, nullptr, rscale, scale, rows};
         GemvIn in{x, nullptr, 0.0f, cols};
@@ -163,11 +164,12 @@ static int mha_launch_hd(const float* q, const KT* kc, const KT* vc, float* out,
                          int T, int H, int Hkv, long long pos_stride, long long head_stride, long long layer_stride,
                          float* part, hipStream_t s) {
     using Geo = AttnGeom<KT, HD>;
-    const int max_splits = (T + Geo::PPW - 1) / Geo::PPW;
+    constexpr int ppw_wg = kAttnWaves * Geo::PPW;
+    const int wg_splits = (T + ppw_wg - 1) / ppw_wg;
+    if (wg_splits > kAttnMaxWgSplits) return fail(SLI_ERR_SHAPE, "mha: context too long for the combine kernel");
     AttnArgs<KT> a{q, kc + (long long)layer * layer_stride, vc + (long long)layer * layer_stride, pos_stride,
-                   head_stride, part, pos_dev, pos, Hkv, max_splits, 1.0f / sqrtf((float)HD)};
-    const int waves = Hkv * max_splits;
-    const int blocks = (waves + 3) / 4;
+                   head_stride, part, pos_dev, pos, Hkv, wg_splits, 1.0f / sqrtf((float)HD)};
+    const int blocks = Hkv * wg_splits;
     const int g = H / Hkv;
     switch (g) {
         case 1: hipLaunchKernelGGL((attn_partial_kernel<KT, HD, 1>), dim3(blocks), dim3(256), 0, s, a); break;
@@ -177,8 +179,8 @@ static int mha_launch_hd(const float* q, const KT* kc, const KT* vc, float* out,
         default: return fail(SLI_ERR_SHAPE, "mha: heads per kv head must be 1, 2, 4 or 8");
     }
     SLI_HIP(hipGetLastError());
-    hipLaunchKernelGGL((attn_combine_kernel<HD>), dim3(H), dim3(64), 0, s, part, out, pos_dev, pos, max_splits,
-                       Geo::PPW);
+    hipLaunchKernelGGL((attn_combine_kernel<HD>), dim3(H), dim3(128), 0, s, part, out, pos_dev, pos, wg_splits,
+                       ppw_wg);
     SLI_HIP(hipGetLastError());
     return SLI_OK;
 }
@@ -202,8 +204,8 @@ template int mha_launch<__half>(const float*, const __half*, const __half*, floa
                                 int, int, int, long long, long long, long long, float*, hipStream_t);
 
 size_t mha_workspace_bytes(int T, int H, int hd) {
-    const int ppw_min = mha_ppw(SLI_DT_F32, hd);
-    const size_t splits = (size_t)((T + ppw_min - 1) / ppw_min);
+    const int ppw_wg_min = kAttnWaves * mha_ppw(SLI_DT_F32, hd);
+    const size_t splits = (size_t)((T + ppw_wg_min - 1) / ppw_wg_min);
     return sizeof(float) * (size_t)H * splits * (size_t)(hd + 2);
 }
 
