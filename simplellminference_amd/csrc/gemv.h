@@ -89,14 +89,18 @@ __device__ __forceinline__ void gemv_stage_x(float* smem, const GemvIn& in) {
     }
 }
 
-// acc[r] += sum over the U vectors (64 lanes apart, starting at vector index v) of W[r] . x
-template <typename WT, int R, int U>
-__device__ __forceinline__ void gemv_chunk(const u32x4 (&w)[U][R], const float* xs, int v, float* acc) {
+// acc[r] += sum over the U vectors (64 lanes apart, starting at vector index v) of W[r] . x.
+// MASK: vectors at index >= nvec contribute nothing (their loads were clamped in range by the caller).
+template <typename WT, int R, int U, bool MASK = false>
+__device__ __forceinline__ void gemv_chunk(const u32x4 (&w)[U][R], const float* xs, int v, float* acc,
+                                           int nvec = 0) {
     constexpr int EPV = Vec16<WT>::N;
 #pragma unroll
     for (int j = 0; j < U; ++j) {
+        const int vj = v + j * 64;
+        if (MASK && vj >= nvec) continue;
         float xv[EPV];
-        const float4* xp = reinterpret_cast<const float4*>(xs + (size_t)(v + j * 64) * EPV);
+        const float4* xp = reinterpret_cast<const float4*>(xs + (size_t)vj * EPV);
 #pragma unroll
         for (int e = 0; e < EPV / 4; ++e) {
             float4 t = xp[e];
@@ -174,11 +178,15 @@ __global__ void __launch_bounds__(kGemvThreads) gemv_kernel(const WT* __restrict
                 for (int r = 0; r < R; ++r) w[j][r] = load16<NT>(wp[r] + (size_t)(v + j * 64) * 16);
             gemv_chunk<WT, R, U>(w, xs, v, acc);
         }
-        for (; v < nvec; v += 64) {
-            u32x4 w[1][R];
+        if (v < nvec) {  // remainder (< U*64 vectors): one masked chunk, all loads in flight together
+            u32x4 w[U][R];
 #pragma unroll
-            for (int r = 0; r < R; ++r) w[0][r] = load16<NT>(wp[r] + (size_t)v * 16);
-            gemv_chunk<WT, R, 1>(w, xs, v, acc);
+            for (int j = 0; j < U; ++j) {
+                const int vj = min(v + j * 64, nvec - 1);  // clamp, never branch around a load
+#pragma unroll
+                for (int r = 0; r < R; ++r) w[j][r] = load16<NT>(wp[r] + (size_t)vj * 16);
+            }
+            gemv_chunk<WT, R, U, true>(w, xs, v, acc, nvec);
         }
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r] = wave_sum(acc[r]);
