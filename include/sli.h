@@ -121,6 +121,18 @@ typedef struct {
 
 typedef struct sli_model sli_model;
 
+/* Tensor-parallel shard plan (host only, no device needed): the window of the full reference-layout
+ * tensor `kind` (sli_synth.h) that rank cfg->tp_rank holds, and where it lands in the rank's fused
+ * buffer. Megatron split: wq/wk/wv/gate/up by output rows (heads / FFN columns),
+ * wo/down by input columns, embedding and norms replicated, LM head = embedding rows [vocab_lo,
+ * vocab_lo + vocab_n). */
+typedef struct {
+    int32_t row_lo, n_rows, col_lo, n_cols, full_cols;
+    int32_t dst_row_off; /* first row inside the rank's fused buffer ([q;k;v] or [gate;up]) */
+} sli_shard_window;
+int sli_tp_plan(const sli_model_config* cfg, int32_t kind, sli_shard_window* out);
+int sli_tp_vocab(const sli_model_config* cfg, int32_t* vocab_lo, int32_t* vocab_n);
+
 /* RCCL unique id for tensor parallelism (broadcast it from rank 0 with any host transport). */
 int sli_comm_id_bytes(void);
 int sli_comm_get_id(void* out);
@@ -155,6 +167,9 @@ int sli_model_predict(sli_model* m, const int32_t* prompt, int32_t n_prompt, int
 /* Copy one layer's K (which=0) or V (which=1) cache, positions [0, upto), to host as fp32 in reference
  * layout [upto][KV_local]. */
 int sli_model_get_kv(sli_model* m, int32_t layer, int32_t which, int32_t upto, float* host);
+/* Read back this rank's shard of a weight (sli_tp_plan window, n = n_rows * n_cols) as fp32 (int8 is
+ * dequantised with its row scales). */
+int sli_model_get_weight(sli_model* m, int32_t kind, int32_t index, float* host, int64_t n);
 int sli_model_stream(sli_model* m, sli_stream_t* out);
 /* Algorithmic HBM bytes of one step on this rank (weights, KV at the current position) — SURVEY.md §8(d). */
 int sli_model_step_bytes(sli_model* m, double* weight_bytes, double* kv_bytes);

@@ -35,6 +35,10 @@ class ModelConfig(ctypes.Structure):
                [(n, c_i32) for n in ("w_dtype", "kv_dtype", "act_mode", "tp_rank", "tp_size", "device")]
 
 
+class ShardWindow(ctypes.Structure):
+    _fields_ = [(n, c_i32) for n in ("row_lo", "n_rows", "col_lo", "n_cols", "full_cols", "dst_row_off")]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "sli_version": (c_int, []),
@@ -62,6 +66,8 @@ _SIGS = {
     "sli_add": (c_int, [c_vp, c_vp, c_vp, c_i32, c_vp]),
     "sli_embedding": (c_int, [c_i32, c_vp, c_vp, c_int, c_vp, c_vp, c_i32, c_i32, c_vp]),
     "sli_argmax": (c_int, [c_vp, c_i32, c_vp, c_vp]),
+    "sli_tp_plan": (c_int, [ctypes.POINTER(ModelConfig), c_i32, ctypes.POINTER(ShardWindow)]),
+    "sli_tp_vocab": (c_int, [ctypes.POINTER(ModelConfig), P_i32, P_i32]),
     "sli_comm_id_bytes": (c_int, []),
     "sli_comm_get_id": (c_int, [c_vp]),
     "sli_model_create": (c_int, [ctypes.POINTER(ModelConfig), c_vp, ctypes.POINTER(c_vp)]),
@@ -79,6 +85,7 @@ _SIGS = {
     "sli_model_get_logits": (c_int, [c_vp, c_vp, c_i32, P_i32]),
     "sli_model_predict": (c_int, [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp]),
     "sli_model_get_kv": (c_int, [c_vp, c_i32, c_i32, c_i32, c_vp]),
+    "sli_model_get_weight": (c_int, [c_vp, c_i32, c_i32, c_vp, c_i64]),
     "sli_model_stream": (c_int, [c_vp, ctypes.POINTER(c_vp)]),
     "sli_model_step_bytes": (c_int, [c_vp, P_d, P_d]),
     "sli_model_time_gemv": (c_int, [c_vp, c_i32, P_d, P_d, P_i32]),

@@ -18,6 +18,7 @@
 #include <unistd.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -57,6 +58,8 @@ struct sli_model {
     sli_model_config c{};
     hipStream_t stream = nullptr;
     ncclComm_t comm = nullptr;
+    bool partial = false;    // wo/down write per-rank partials (+ residual on rank 0) into xpart
+    bool collectives = false;  // all-reduce partials / argmax keys over RCCL inside the step
     // local (this rank's) geometry
     int D = 0, L = 0, T = 0, V = 0, hd = 0, hq = 0, hkv = 0, Il = 0;
     int v_lo = 0, v_n = 0;
@@ -178,41 +181,32 @@ static int place_f32(sli_model* m, float* dst, int n, const Src& src) {
 
 static char* wptr(void* base, size_t elem_bytes, size_t elems) { return (char*)base + elem_bytes * elems; }
 
-// Place one full reference tensor (kind, index) from `src` into this rank's shard(s).
+// Place one full reference tensor (kind, index) from `src` into this rank's shard (sli_tp_plan).
 template <class Src>
 static int place_tensor(sli_model* m, int kind, int index, const Src& src) {
-    const int D = m->D, hd = m->hd, r = m->c.tp_rank;
-    const int Ifull = m->c.ffn;
-    const size_t wb = m->wbytes;
-    if (kind == SLI_T_EMB) return place(m, m->emb, m->emb_s, m->V, D, 0, 0, D, src);
+    const int D = m->D;
     if (kind == SLI_T_NORM) {
         if (index < 0 || index > 2 * m->L) return fail(SLI_ERR_RANGE, "norm index");
         return place_f32(m, m->norms + (size_t)index * D, D, src);
     }
+    sli_shard_window w;
+    SLI_TRY(sli_tp_plan(&m->c, kind, &w));
+    if (kind == SLI_T_EMB)
+        return place(m, m->emb, m->emb_s, w.n_rows, w.n_cols, w.row_lo, w.col_lo, w.full_cols, src);
     if (index < 0 || index >= m->L) return fail(SLI_ERR_RANGE, "layer index");
-    LayerW& w = m->layers[index];
-    const int qr = m->hq * hd, kr = m->hkv * hd;
+    LayerW& L = m->layers[index];
+    void* base = nullptr;
+    float* sbase = nullptr;
     switch (kind) {
-        case SLI_T_WQ:
-            return place(m, w.qkv, w.qkv_s, qr, D, r * qr, 0, D, src);
-        case SLI_T_WK:
-            return place(m, wptr(w.qkv, wb, (size_t)qr * D), w.qkv_s ? w.qkv_s + qr : nullptr, kr, D, r * kr, 0, D,
-                         src);
-        case SLI_T_WV:
-            return place(m, wptr(w.qkv, wb, (size_t)(qr + kr) * D), w.qkv_s ? w.qkv_s + qr + kr : nullptr, kr, D,
-                         r * kr, 0, D, src);
-        case SLI_T_WO:
-            return place(m, w.wo, w.wo_s, D, qr, 0, r * qr, D, src);
-        case SLI_T_GATE:
-            return place(m, w.gu, w.gu_s, m->Il, D, r * m->Il, 0, D, src);
-        case SLI_T_UP:
-            return place(m, wptr(w.gu, wb, (size_t)m->Il * D), w.gu_s ? w.gu_s + m->Il : nullptr, m->Il, D,
-                         r * m->Il, 0, D, src);
-        case SLI_T_DOWN:
-            return place(m, w.down, w.down_s, D, m->Il, 0, r * m->Il, Ifull, src);
-        default:
-            return fail(SLI_ERR_ARG, "unknown tensor kind");
+        case SLI_T_WQ: case SLI_T_WK: case SLI_T_WV: base = L.qkv; sbase = L.qkv_s; break;
+        case SLI_T_WO: base = L.wo; sbase = L.wo_s; break;
+        case SLI_T_GATE: case SLI_T_UP: base = L.gu; sbase = L.gu_s; break;
+        case SLI_T_DOWN: base = L.down; sbase = L.down_s; break;
+        default: return fail(SLI_ERR_ARG, "unknown tensor kind");
     }
+    void* dst = wptr(base, m->wbytes, (size_t)w.dst_row_off * w.n_cols);
+    return place(m, dst, sbase ? sbase + w.dst_row_off : nullptr, w.n_rows, w.n_cols, w.row_lo, w.col_lo,
+                 w.full_cols, src);
 }
 
 static int64_t tensor_elems(const sli_model* m, int kind) {
@@ -308,7 +302,7 @@ struct StepRecorder {
     }
     static int gemv_wo(sli_model* m, int l) {
         const LayerW& w = m->layers[l];
-        const bool tp = m->c.tp_size > 1;
+        const bool tp = m->partial;
         GemvIn in{m->attn, nullptr, 0.0f, m->hq * m->hd};
         EpiStore<2> e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, w.wo_s, 1.0f, m->D};
         SLI_HIP((launch_gemv<WT, 2, 8, NT>((const WT*)w.wo, in, e, (m->D + 1) / 2, m->stream)));
@@ -323,7 +317,7 @@ struct StepRecorder {
     }
     static int gemv_down(sli_model* m, int l) {
         const LayerW& w = m->layers[l];
-        const bool tp = m->c.tp_size > 1;
+        const bool tp = m->partial;
         GemvIn in{m->act, nullptr, 0.0f, m->Il};
         EpiStore<2> e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, w.down_s, 1.0f, m->D};
         SLI_HIP((launch_gemv<WT, 2, 8, NT>((const WT*)w.down, in, e, (m->D + 1) / 2, m->stream)));
@@ -338,7 +332,10 @@ struct StepRecorder {
         return SLI_OK;
     }
     static int allreduce_x(sli_model* m) {
-        if (m->c.tp_size > 1) SLI_NCCL(ncclAllReduce(m->xpart, m->x, m->D, ncclFloat32, ncclSum, m->comm, m->stream));
+        if (m->collectives)
+            SLI_NCCL(ncclAllReduce(m->xpart, m->x, m->D, ncclFloat32, ncclSum, m->comm, m->stream));
+        else if (m->partial)  // debug no-comm mode: keep the local partial as the residual stream
+            SLI_HIP(hipMemcpyAsync(m->x, m->xpart, sizeof(float) * m->D, hipMemcpyDeviceToDevice, m->stream));
         return SLI_OK;
     }
     static int record(sli_model* m) {
@@ -358,8 +355,7 @@ struct StepRecorder {
         SLI_TRY(gemv_lm(m));
         hipLaunchKernelGGL(keyreduce_kernel, dim3(1), dim3(256), 0, s, m->keys, lm_head_blocks(m), m->st);
         SLI_HIP(hipGetLastError());
-        if (m->c.tp_size > 1)
-            SLI_NCCL(ncclAllReduce(&m->st->key, &m->st->key, 1, ncclUint64, ncclMax, m->comm, s));
+        if (m->collectives) SLI_NCCL(ncclAllReduce(&m->st->key, &m->st->key, 1, ncclUint64, ncclMax, m->comm, s));
         hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1), 0, s, m->st, m->prompt, m->hist, m->T);
         SLI_HIP(hipGetLastError());
         return SLI_OK;
@@ -475,7 +471,8 @@ int sli_model_create(const sli_model_config* cfg, const void* comm_id, sli_model
     SLI_CHECK((c.ffn / c.tp_size) % 2 == 0, SLI_ERR_SHAPE, "local ffn must be even");
     SLI_CHECK(c.w_dtype >= SLI_DT_F32 && c.w_dtype <= SLI_DT_I8, SLI_ERR_ARG, "bad w_dtype");
     SLI_CHECK(c.kv_dtype == SLI_DT_F32 || c.kv_dtype == SLI_DT_F16, SLI_ERR_ARG, "bad kv_dtype");
-    SLI_CHECK(c.tp_size == 1 || comm_id, SLI_ERR_ARG, "tensor parallel needs a comm id");
+    SLI_CHECK(c.tp_size == 1 || comm_id || std::getenv("SLI_DEBUG_NOCOMM"), SLI_ERR_ARG,
+              "tensor parallel needs a comm id");
     const size_t wb = c.w_dtype == SLI_DT_F32 ? 4 : c.w_dtype == SLI_DT_F16 ? 2 : 1;
     SLI_CHECK(((size_t)c.dim * wb) % 16 == 0 && ((size_t)(c.ffn / c.tp_size) * wb) % 16 == 0 &&
                   ((size_t)(c.dim / c.tp_size) * wb) % 16 == 0,
@@ -499,9 +496,10 @@ int sli_model_create(const sli_model_config* cfg, const void* comm_id, sli_model
     m->hq = c.n_heads / c.tp_size;
     m->hkv = c.n_kv_heads / c.tp_size;
     m->Il = c.ffn / c.tp_size;
-    const int vchunk = (c.vocab + c.tp_size - 1) / c.tp_size;
-    m->v_lo = c.tp_rank * vchunk;
-    m->v_n = std::max(0, std::min(vchunk, c.vocab - m->v_lo));
+    int32_t vlo = 0, vn = 0;
+    if (sli_tp_vocab(&c, &vlo, &vn) != SLI_OK) return bail(SLI_ERR_ARG);
+    m->v_lo = vlo;
+    m->v_n = vn;
     if (m->v_n <= 0) return bail(fail(SLI_ERR_SHAPE, "vocab shard is empty"));
     m->wbytes = wb;
     m->kvbytes = c.kv_dtype == SLI_DT_F32 ? 4 : 2;
@@ -556,9 +554,20 @@ int sli_model_create(const sli_model_config* cfg, const void* comm_id, sli_model
         return bail(fail(SLI_ERR_HIP, "memset"));
     if ((rc = sli_model_reset(m)) != SLI_OK) return bail(rc);
 
-    if (c.tp_size > 1) {
+    // Debug switches (tests only): SLI_DEBUG_FORCE_COMM=1 runs the tensor-parallel step
+    // (partials + RCCL all-reduces) on a 1-rank communicator; SLI_DEBUG_NOCOMM=1 builds a tp_size>1
+    // shard without a communicator (weight-placement checks; its logits are not meaningful).
+    const bool force_comm = c.tp_size == 1 && std::getenv("SLI_DEBUG_FORCE_COMM") != nullptr;
+    const bool no_comm = c.tp_size > 1 && std::getenv("SLI_DEBUG_NOCOMM") != nullptr;
+    m->partial = c.tp_size > 1 || force_comm;
+    m->collectives = (c.tp_size > 1 && !no_comm) || force_comm;
+    if (m->collectives) {
         ncclUniqueId id;
-        std::memcpy(&id, comm_id, sizeof(id));
+        if (comm_id) {
+            std::memcpy(&id, comm_id, sizeof(id));
+        } else if (ncclGetUniqueId(&id) != ncclSuccess) {
+            return bail(fail(SLI_ERR_COMM, "ncclGetUniqueId"));
+        }
         ncclResult_t r = ncclCommInitRank(&m->comm, c.tp_size, id, c.tp_rank);
         if (r != ncclSuccess) return bail(fail(SLI_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r)));
     }
@@ -746,6 +755,61 @@ int sli_model_get_kv(sli_model* m, int32_t layer, int32_t which, int32_t upto, f
     if (hipStreamSynchronize(m->stream) != hipSuccess && rc == SLI_OK) rc = fail(SLI_ERR_HIP, "sync");
     (void)hipFree(tmp);
     return rc;
+}
+
+int sli_model_get_weight(sli_model* m, int32_t kind, int32_t index, float* host, int64_t n) {
+    SLI_CHECK(m && host, SLI_ERR_ARG, "null argument");
+    const void* src = nullptr;
+    const float* scale = nullptr;
+    int64_t rows = 0, cols = 0;
+    if (kind == SLI_T_NORM) {
+        SLI_CHECK(index >= 0 && index <= 2 * m->L, SLI_ERR_RANGE, "norm index");
+        SLI_CHECK(n == m->D, SLI_ERR_SHAPE, "host buffer size");
+        SLI_HIP(hipMemcpy(host, m->norms + (size_t)index * m->D, sizeof(float) * m->D, hipMemcpyDeviceToHost));
+        return SLI_OK;
+    }
+    sli_shard_window w;
+    SLI_TRY(sli_tp_plan(&m->c, kind, &w));
+    rows = w.n_rows;
+    cols = w.n_cols;
+    if (kind == SLI_T_EMB) {
+        src = m->emb;
+        scale = m->emb_s;
+    } else {
+        SLI_CHECK(index >= 0 && index < m->L, SLI_ERR_RANGE, "layer index");
+        const LayerW& L = m->layers[index];
+        switch (kind) {
+            case SLI_T_WQ: case SLI_T_WK: case SLI_T_WV: src = L.qkv; scale = L.qkv_s; break;
+            case SLI_T_WO: src = L.wo; scale = L.wo_s; break;
+            case SLI_T_GATE: case SLI_T_UP: src = L.gu; scale = L.gu_s; break;
+            case SLI_T_DOWN: src = L.down; scale = L.down_s; break;
+            default: return fail(SLI_ERR_ARG, "unknown tensor kind");
+        }
+        src = wptr(const_cast<void*>(src), m->wbytes, (size_t)w.dst_row_off * w.n_cols);
+        if (scale) scale += w.dst_row_off;
+    }
+    SLI_CHECK(n == rows * cols, SLI_ERR_SHAPE, "host buffer size must be the local shard's rows*cols");
+    std::vector<unsigned char> raw((size_t)(rows * cols) * m->wbytes);
+    SLI_HIP(hipMemcpy(raw.data(), src, raw.size(), hipMemcpyDeviceToHost));
+    std::vector<float> sc;
+    if (scale) {
+        sc.resize(rows);
+        SLI_HIP(hipMemcpy(sc.data(), scale, sizeof(float) * rows, hipMemcpyDeviceToHost));
+    }
+    for (int64_t i = 0; i < rows * cols; ++i) {
+        float v;
+        if (m->wbytes == 4) {
+            std::memcpy(&v, &raw[4 * i], 4);
+        } else if (m->wbytes == 2) {
+            __half h;
+            std::memcpy(&h, &raw[2 * i], 2);
+            v = __half2float(h);
+        } else {
+            v = (float)(int8_t)raw[i] * sc[i / cols];
+        }
+        host[i] = v;
+    }
+    return SLI_OK;
 }
 
 int sli_model_stream(sli_model* m, sli_stream_t* out) {

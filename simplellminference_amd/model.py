@@ -160,6 +160,19 @@ class LlamaModel:
              toks.ctypes.data_as(ctypes.c_void_p), logits.ctypes.data_as(ctypes.c_void_p) if want_logits else None)
         return (toks, logits) if want_logits else toks
 
+    def weight_shard(self, kind: int, index: int = 0) -> np.ndarray:
+        """This rank's shard of a weight (sli_tp_plan window) read back as fp32."""
+        from .tp import KINDS, shard_window
+        name = {v: k for k, v in KINDS.items()}[kind]
+        if name == "norm":
+            shape = (self.config.hidden_size,)
+        else:
+            w = shard_window(self.config, name, self.tp_rank, self.tp_size)
+            shape = (w.n_rows, w.n_cols)
+        out = np.empty(shape, np.float32)
+        call("sli_model_get_weight", self._h, kind, index, out.ctypes.data_as(ctypes.c_void_p), out.size)
+        return out
+
     def kv(self, layer: int, which: int, upto: int) -> np.ndarray:
         c = self.config
         out = np.empty((upto, c.num_key_value_heads // self.tp_size * c.head_dim), np.float32)
