@@ -23,7 +23,7 @@ struct AttnArgs {
     const KT* v;
     long long pos_stride;   // elements between positions
     long long head_stride;  // elements between kv heads
-    float* part;            // [hq][max_splits][hd + 2]
+    float* part;            // [hq][max_splits][hd + kAttnPartPad]: o[hd], m, l, pad
     const int32_t* pos_dev; // nullable: then pos_host
     int pos_host;
     int n_kv_heads;
@@ -158,7 +158,7 @@ __global__ void __launch_bounds__(256) attn_partial_kernel(AttnArgs<KT> a) {
             o = fmaf(c, sh[w][g][d], o);
             L = fmaf(c, sh[w][g][HD + 1], L);
         }
-        float* dst = a.part + ((size_t)(kvh * G + g) * a.max_splits + wgs) * (HD + 2);
+        float* dst = a.part + ((size_t)(kvh * G + g) * a.max_splits + wgs) * (HD + kAttnPartPad);
         dst[d] = o;
         if (d == 0) {
             dst[HD] = M;
@@ -178,16 +178,17 @@ __global__ void __launch_bounds__(256)
     const int tid = threadIdx.x;
     const int pos = pos_dev ? *pos_dev : pos_host;
     const int ns = pos / ppw_wg + 1;
-    const float* ph = part + (size_t)h * max_splits * (HD + 2);
+    constexpr int PS = HD + kAttnPartPad;
+    const float* ph = part + (size_t)h * max_splits * PS;
     if (tid < 64) {
         float mx = -INFINITY;
-        for (int i = tid; i < ns; i += 64) mx = fmaxf(mx, ph[(size_t)i * (HD + 2) + HD]);
+        for (int i = tid; i < ns; i += 64) mx = fmaxf(mx, ph[(size_t)i * PS + HD]);
         mx = wave_max(mx);
         float L = 0.0f;
         for (int i = tid; i < ns; i += 64) {
-            const float w = expf(ph[(size_t)i * (HD + 2) + HD] - mx);
+            const float w = expf(ph[(size_t)i * PS + HD] - mx);
             sw[i] = w;
-            L = fmaf(w, ph[(size_t)i * (HD + 2) + HD + 1], L);
+            L = fmaf(w, ph[(size_t)i * PS + HD + 1], L);
         }
         L = wave_sum(L);
         if (tid == 0) sL = L;
@@ -197,7 +198,7 @@ __global__ void __launch_bounds__(256)
     for (int d = tid; d < HD; d += blockDim.x) {
         float o = 0.0f;
 #pragma unroll 8
-        for (int i = 0; i < ns; ++i) o = fmaf(sw[i], ph[(size_t)i * (HD + 2) + d], o);
+        for (int i = 0; i < ns; ++i) o = fmaf(sw[i], ph[(size_t)i * PS + d], o);
         out[(size_t)h * HD + d] = o / L;
     }
 }

@@ -12,6 +12,8 @@
 namespace sli {
 
 constexpr int kWave = 64;  // CDNA wavefront; never 32 (MI355X_MICROARCH.md "wave = 64 not 32")
+// Split-context attention partial row: o[hd], m, l, 2 pad floats (16-B aligned rows for float4 merges).
+constexpr int kAttnPartPad = 4;
 
 // ---------------------------------------------------------------- error plumbing (host)
 void set_error(const std::string& msg);

@@ -19,6 +19,7 @@
 
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 #include <cstring>
 #include <vector>
 
@@ -27,19 +28,11 @@
 #include "common.h"
 #include "gemv.h"
 #include "ops_internal.h"
+#include "persistent.h"
+#include "persistent_launch.h"
 #include "rope_table.h"
 
 namespace sli {
-
-struct DevState {
-    int32_t pos;          // position of the token being fed
-    int32_t token;        // token fed at pos
-    int32_t n_forced;     // prompt length (teacher forcing while pos < n_forced)
-    int32_t last_argmax;  // greedy argmax of the last step's logits
-    int32_t advance;      // 1: finalize advances pos/token; 0: idempotent step (bench)
-    int32_t error;
-    unsigned long long key;  // argmax key of the last step (0 between steps)
-};
 
 struct LayerW {
     void* qkv = nullptr;   // [(hq + 2 hkv) hd][D]
@@ -78,6 +71,14 @@ struct sli_model {
     sli::DevState* st = nullptr;
     int32_t* prompt = nullptr;
     int32_t* hist = nullptr;
+    // persistent step (persistent.h)
+    bool persistent = false;
+    int grid = 256;                          // one 1024-thread workgroup per CU
+    size_t step_lds = 0;
+    sli::StepParams* dparams = nullptr;      // device copy of the step parameters
+    sli::LayerPtrs* dlayers = nullptr;
+    unsigned* bar = nullptr;                 // grid-barrier words, zeroed before every launch
+    unsigned long long* stamps = nullptr;    // SLI_DEBUG_STAMPS: per-phase s_memrealtime (100 MHz)
     hipGraph_t graph = nullptr;
     hipGraphExec_t graph_exec = nullptr;
     std::vector<void*> allocs;
@@ -244,20 +245,8 @@ __global__ void keyreduce_kernel(const unsigned long long* __restrict__ keys, in
     }
 }
 
-// model.cpp:157-183: next position; teacher-forced prompt token while inside the prompt, else greedy.
 __global__ void finalize_kernel(DevState* st, const int32_t* __restrict__ prompt, int32_t* hist, int T) {
-    const unsigned long long k = st->key;
-    const int next = (int)argmax_key_index(k);
-    st->last_argmax = next;
-    st->key = 0;
-    if (st->advance) {
-        const int p = st->pos + 1;
-        if (p < T) {
-            st->pos = p;
-            st->token = p < st->n_forced ? prompt[p] : next;
-            hist[p] = st->token;
-        }
-    }
+    finalize_state(st, prompt, hist, T);
 }
 
 template <typename KT>
@@ -300,12 +289,28 @@ struct StepRecorder {
         SLI_HIP((launch_gemv<WT, 2, 8, NT>((const WT*)w.qkv, in, e, (m->hq + 2 * m->hkv) * (m->hd / 2), m->stream)));
         return SLI_OK;
     }
-    static int gemv_wo(sli_model* m, int l) {
+    static bool fused_combine_fits(const sli_model* m) {
+        const int ppw = attn_wg_positions(m->c.kv_dtype, m->hd);
+        const size_t ml = sizeof(float) * 2 * (size_t)m->hq * ((m->T + ppw - 1) / ppw);
+        return gemv_lds_bytes(m->hq * m->hd) + ml <= 65536;
+    }
+    static int gemv_wo(sli_model* m, int l, bool fused_combine = false) {
         const LayerW& w = m->layers[l];
         const bool tp = m->partial;
         GemvIn in{m->attn, nullptr, 0.0f, m->hq * m->hd};
+        if (fused_combine) {  // merge the attention partials in the prologue (no combine launch)
+            const int ppw = attn_wg_positions(m->c.kv_dtype, m->hd);
+            in.part = m->part;
+            in.pos = &m->st->pos;
+            in.hd = m->hd;
+            in.ppw_wg = ppw;
+            in.max_splits = (m->T + ppw - 1) / ppw;
+        }
         EpiStore<2> e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, w.wo_s, 1.0f, m->D};
-        SLI_HIP((launch_gemv<WT, 2, 8, NT>((const WT*)w.wo, in, e, (m->D + 1) / 2, m->stream)));
+        if (fused_combine)
+            SLI_HIP((launch_gemv<WT, 2, 8, NT, true>((const WT*)w.wo, in, e, (m->D + 1) / 2, m->stream)));
+        else
+            SLI_HIP((launch_gemv<WT, 2, 8, NT>((const WT*)w.wo, in, e, (m->D + 1) / 2, m->stream)));
         return SLI_OK;
     }
     static int gemv_gu(sli_model* m, int l) {
@@ -338,15 +343,45 @@ struct StepRecorder {
             SLI_HIP(hipMemcpyAsync(m->x, m->xpart, sizeof(float) * m->D, hipMemcpyDeviceToDevice, m->stream));
         return SLI_OK;
     }
+    // ---- persistent step (persistent.h): instantiated for the common storage pairs and head shapes
+    static bool persistent_ok(const sli_model* m) {
+        return persistent_supported(m->c.w_dtype, m->c.kv_dtype, m->hd, m->hq / m->hkv);
+    }
+    static int persist(sli_model* m, int pb, int pe, int fin) {
+        return persistent_launch(m->c.w_dtype, m->c.kv_dtype, m->hd, m->hq / m->hkv, m->dparams, m->grid,
+                                 m->step_lds, m->bar, pb, pe, fin, m->stream);
+    }
+    static int record_persistent(sli_model* m) {
+        const int last = m->L * kPhasesPerLayer;
+        if (!m->partial) return persist(m, 0, last + 1, 1);  // the whole step is one launch
+        for (int l = 0; l < m->L; ++l) {                     // TP: cut at the two all-reduces per layer
+            SLI_TRY(persist(m, l * kPhasesPerLayer, l * kPhasesPerLayer + kPhGU, 0));
+            SLI_TRY(allreduce_x(m));
+            SLI_TRY(persist(m, l * kPhasesPerLayer + kPhGU, (l + 1) * kPhasesPerLayer, 0));
+            SLI_TRY(allreduce_x(m));
+        }
+        SLI_TRY(persist(m, last, last + 1, 0));
+        hipStream_t s = m->stream;
+        hipLaunchKernelGGL(keyreduce_kernel, dim3(1), dim3(256), 0, s, m->keys, m->grid, m->st);
+        SLI_HIP(hipGetLastError());
+        if (m->collectives) SLI_NCCL(ncclAllReduce(&m->st->key, &m->st->key, 1, ncclUint64, ncclMax, m->comm, s));
+        hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1), 0, s, m->st, m->prompt, m->hist, m->T);
+        SLI_HIP(hipGetLastError());
+        return SLI_OK;
+    }
+    static int uses_persistent(sli_model* m) { return m->persistent && persistent_ok(m) ? 1 : 0; }
+
     static int record(sli_model* m) {
+        if (m->persistent && persistent_ok(m)) return record_persistent(m);
         hipStream_t s = m->stream;
         SLI_TRY(embedding_launch(0, &m->st->token, m->emb, m->c.w_dtype, m->emb_s, m->x, m->V, m->D, s));
         const long long ps = m->hd, hs = (long long)m->T * m->hd, ls = (long long)m->hkv * m->T * m->hd;
+        const bool fuse = fused_combine_fits(m);  // split merge inside the wo GEMV prologue
         for (int l = 0; l < m->L; ++l) {
             SLI_TRY(gemv_qkv(m, l));
             SLI_TRY(mha_launch<KT>(m->q, (const KT*)m->kc, (const KT*)m->vc, m->attn, l, 0, &m->st->pos, m->T, m->hd,
-                                   m->hq, m->hkv, ps, hs, ls, m->part, s));
-            SLI_TRY(gemv_wo(m, l));
+                                   m->hq, m->hkv, ps, hs, ls, m->part, s, /*combine=*/!fuse));
+            SLI_TRY(gemv_wo(m, l, fuse));
             SLI_TRY(allreduce_x(m));
             SLI_TRY(gemv_gu(m, l));
             SLI_TRY(gemv_down(m, l));
@@ -535,7 +570,12 @@ int sli_model_create(const sli_model_config* cfg, const void* comm_id, sli_model
     A((void**)&m->attn, sizeof(float) * m->hq * hd);
     A((void**)&m->act, sizeof(float) * m->Il);
     A((void**)&m->logits, sizeof(float) * m->v_n);
-    A((void**)&m->part, mha_workspace_bytes(m->T, m->hq, hd));
+    {  // split-context partials [hq][splits][hd + kAttnPartPad] (launch and persistent paths)
+        const int ppw_wg_f32 = pattn_ppw_wg(hd, 4, 4);  // smallest persistent slice (f32 KV, GQA-4)
+        const size_t persist_bytes =
+            sizeof(float) * (size_t)m->hq * ((m->T + ppw_wg_f32 - 1) / ppw_wg_f32) * (hd + kPartStride);
+        A((void**)&m->part, std::max(mha_workspace_bytes(m->T, m->hq, hd), persist_bytes));
+    }
     A((void**)&m->sin_t, sizeof(float) * (size_t)m->T * (hd / 2));
     A((void**)&m->cos_t, sizeof(float) * (size_t)m->T * (hd / 2));
     A((void**)&m->keys, sizeof(unsigned long long) * kGemvMaxBlocks);
@@ -561,6 +601,53 @@ int sli_model_create(const sli_model_config* cfg, const void* comm_id, sli_model
     const bool no_comm = c.tp_size > 1 && std::getenv("SLI_DEBUG_NOCOMM") != nullptr;
     m->partial = c.tp_size > 1 || force_comm;
     m->collectives = (c.tp_size > 1 && !no_comm) || force_comm;
+
+    // persistent-step parameters (persistent.h)
+    {
+        // Default: one launch per fused op (measured faster); SLI_STEP_MODE=persistent runs the
+        // whole step as one persistent launch with grid barriers (persistent.h, experimental).
+        const char* mode = std::getenv("SLI_STEP_MODE");
+        m->persistent = mode && std::string(mode) == "persistent";
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device) != hipSuccess || cus <= 0)
+            cus = kGemvCUs;
+        m->grid = std::min(cus, kGemvMaxBlocks);
+        const int g = m->hq / m->hkv;
+        const size_t xs_floats = (size_t)kGemvLdsHead + std::max(std::max(m->D, m->Il), m->hq * hd);
+        const size_t attn_floats = (size_t)4 * kAttnWaves * g * (hd + 2);
+        m->step_lds = sizeof(float) * std::max(xs_floats, attn_floats);
+        std::vector<LayerPtrs> lp(m->L);
+        for (int l = 0; l < m->L; ++l) {
+            const LayerW& w = m->layers[l];
+            lp[l] = LayerPtrs{w.qkv, w.qkv_s, w.wo, w.wo_s, w.gu, w.gu_s, w.down, w.down_s};
+        }
+        A((void**)&m->dlayers, sizeof(LayerPtrs) * m->L);
+        A((void**)&m->dparams, sizeof(StepParams));
+        A((void**)&m->bar, sizeof(unsigned) * kBarWords);
+        unsigned long long* stamps = nullptr;
+        if (std::getenv("SLI_DEBUG_STAMPS")) A((void**)&stamps, sizeof(unsigned long long) * 3 * (m->L * kPhasesPerLayer + 1));
+        if (rc != SLI_OK) return bail(rc);
+        const int ppw_wg = pattn_ppw_wg(hd, c.kv_dtype == SLI_DT_F16 ? 2 : 4, g);
+        StepParams P{};
+        P.D = m->D; P.L = m->L; P.T = m->T; P.hd = hd; P.hq = m->hq; P.hkv = m->hkv; P.Il = m->Il;
+        P.v_lo = m->v_lo; P.v_n = m->v_n; P.V = m->V;
+        P.silu = c.act_mode; P.partial = m->partial ? 1 : 0; P.rank = c.tp_rank; P.eps = c.eps;
+        P.emb = m->emb; P.emb_s = m->emb_s; P.norms = m->norms; P.layers = m->dlayers;
+        P.kc = m->kc; P.vc = m->vc;
+        P.x = m->x; P.xpart = m->xpart; P.q = m->q; P.act = m->act; P.logits = m->logits; P.part = m->part;
+        P.sin_t = m->sin_t; P.cos_t = m->cos_t; P.keys = m->keys; P.st = m->st; P.prompt = m->prompt;
+        P.hist = m->hist; P.bar = m->bar;
+        P.attn_splits = (m->T + ppw_wg - 1) / ppw_wg;
+        P.stamps = stamps;
+        const char* dbg = std::getenv("SLI_DEBUG_BARRIER");
+        P.debug_flags = dbg ? std::atoi(dbg) : 0;
+        m->stamps = stamps;
+        if (hipMemcpy(m->dlayers, lp.data(), sizeof(LayerPtrs) * m->L, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(m->dparams, &P, sizeof(StepParams), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemset(m->bar, 0, sizeof(unsigned) * kBarWords) != hipSuccess)
+            return bail(fail(SLI_ERR_HIP, "persistent step parameters upload"));
+    }
+
     if (m->collectives) {
         ncclUniqueId id;
         if (comm_id) {
@@ -810,6 +897,16 @@ int sli_model_get_weight(sli_model* m, int32_t kind, int32_t index, float* host,
         host[i] = v;
     }
     return SLI_OK;
+}
+
+int sli_model_debug_stamps(sli_model* m, unsigned long long* host, int32_t n) {
+    SLI_CHECK(m && host, SLI_ERR_ARG, "null argument");
+    SLI_CHECK(m->stamps, SLI_ERR_STATE, "model created without SLI_DEBUG_STAMPS=1");
+    const int32_t have = 3 * (m->L * kPhasesPerLayer + 1);
+    SLI_CHECK(n >= have, SLI_ERR_SHAPE, "host buffer too small");
+    SLI_HIP(hipStreamSynchronize(m->stream));
+    SLI_HIP(hipMemcpy(host, m->stamps, sizeof(unsigned long long) * have, hipMemcpyDeviceToHost));
+    return have;
 }
 
 int sli_model_stream(sli_model* m, sli_stream_t* out) {

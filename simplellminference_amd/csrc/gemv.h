@@ -20,6 +20,11 @@ struct GemvIn {
     const float* norm_w;  // nullptr: plain; else fused RMSNorm weight [cols]
     float eps;
     int cols;
+    // Fused split-context merge (attention.h partials): when part != nullptr, x is not read; the staged
+    // input is x[h*hd + d] = sum_i e^{m_i - M} o_i[d] / sum_i e^{m_i - M} l_i over the live splits of head h.
+    const float* part = nullptr;   // [cols / hd][max_splits][hd + kAttnPartPad]
+    const int32_t* pos = nullptr;  // live splits = *pos / ppw_wg + 1
+    int hd = 0, max_splits = 0, ppw_wg = 0;
 };
 
 constexpr int kGemvThreads = 1024;  // one persistent 16-wave workgroup per CU: x staged once per CU
@@ -33,6 +38,66 @@ constexpr int kGemvStageV4 = 4;  // float4 of x per thread: 1024 threads x 4 x 4
 // loads of x (and of the norm weight) before using any (clamped indices, no branch around a load).
 // All LDS lives in one dynamic array (G17: no static __shared__ in front of the dynamic region, so the
 // b128 reads stay 16-byte aligned). Requires cols % 4 == 0 and 16-byte aligned x / norm_w.
+// Merge the attention partials straight into the staged x (replaces attn_combine_kernel and its launch).
+// The (m, l) pairs of every live split go through LDS once per workgroup; each thread then merges the
+// o rows of its 4 columns, CH splits per batch of loads, with the combine kernel's exact arithmetic:
+// M = max m_i, w_i = e^{m_i - M}, x = (sum_i w_i o_i) / (sum_i w_i l_i), summed in split order.
+// The first batch of o loads is issued before the (m, l) round trip so the two overlap.
+// LDS: the staged x [cols] is followed by the (m, l) table [cols / hd][live splits] (gemv_combine_lds).
+__device__ __forceinline__ void gemv_stage_combine(float* xs, const GemvIn& in) {
+    constexpr int CH = 8;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int ps = in.hd + kAttnPartPad;
+    const int ns = min(*in.pos / in.ppw_wg + 1, in.max_splits);
+    const int n4 = in.cols >> 2;
+    const int nml = (in.cols / in.hd) * ns;
+    float2* mls = reinterpret_cast<float2*>(xs + in.cols);
+    const float* part = in.part;
+    auto row = [&](int h, int i) { return part + ((size_t)h * in.max_splits + i) * ps; };
+
+    float4 po[CH];
+    const int h0 = (tid << 2) / in.hd, d0 = (tid << 2) - h0 * in.hd;
+    if (tid < n4) {
+#pragma unroll
+        for (int j = 0; j < CH; ++j) po[j] = *reinterpret_cast<const float4*>(row(h0, min(j, ns - 1)) + d0);
+    }
+    for (int k = tid; k < nml; k += nt) {
+        const int h = k / ns, i = k - h * ns;
+        mls[k] = *reinterpret_cast<const float2*>(row(h, i) + in.hd);
+    }
+    __syncthreads();
+    for (int c4 = tid; c4 < n4; c4 += nt) {
+        const int h = (c4 << 2) / in.hd, d = (c4 << 2) - h * in.hd;
+        const float2* ml = mls + h * ns;
+        float M = -INFINITY;
+        for (int i = 0; i < ns; ++i) M = fmaxf(M, ml[i].x);
+        float L = 0.0f;
+        float4 o = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        for (int i0 = 0; i0 < ns; i0 += CH) {
+            if (c4 != tid || i0 != 0) {
+#pragma unroll
+                for (int j = 0; j < CH; ++j) po[j] = *reinterpret_cast<const float4*>(row(h, min(i0 + j, ns - 1)) + d);
+            }
+#pragma unroll
+            for (int j = 0; j < CH; ++j) {
+                if (i0 + j < ns) {
+                    const float w = expf(ml[i0 + j].x - M);
+                    o.x = fmaf(w, po[j].x, o.x);
+                    o.y = fmaf(w, po[j].y, o.y);
+                    o.z = fmaf(w, po[j].z, o.z);
+                    o.w = fmaf(w, po[j].w, o.w);
+                    L = fmaf(w, ml[i0 + j].y, L);
+                }
+            }
+        }
+        reinterpret_cast<float4*>(xs)[c4] = make_float4(o.x / L, o.y / L, o.z / L, o.w / L);
+    }
+}
+
+inline size_t gemv_combine_lds(const GemvIn& in) {
+    return sizeof(float2) * (size_t)(in.cols / in.hd) * in.max_splits;
+}
+
 __device__ __forceinline__ void gemv_stage_x(float* smem, const GemvIn& in) {
     float* red = smem;
     float* xs = smem + kGemvLdsHead;
@@ -123,7 +188,8 @@ __device__ __forceinline__ void gemv_chunk(const u32x4 (&w)[U][R], const float* 
 // so no wave is left with a second pass while the rest of the chip idles. The first weight chunk of the
 // wave's first unit is issued BEFORE the x-staging prologue, so the prologue's L2 round trips and
 // barriers overlap the first HBM round trip instead of preceding it.
-template <typename WT, int R, int U, bool NT, class Epi>
+// CMB: stage x by merging attention partials (gemv_stage_combine) instead of reading in.x.
+template <typename WT, int R, int U, bool NT, class Epi, bool CMB = false>
 __global__ void __launch_bounds__(kGemvThreads) gemv_kernel(const WT* __restrict__ W, GemvIn in, Epi epi_in) {
     Epi epi = epi_in;  // mutable per-thread copy (EpiLogits keeps a running key)
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -155,7 +221,10 @@ __global__ void __launch_bounds__(kGemvThreads) gemv_kernel(const WT* __restrict
                 pre[j][r] = load16<NT>(reinterpret_cast<const char*>(W) + (size_t)rows[r] * row_bytes +
                                        (size_t)(lane + j * 64) * 16);
     }
-    gemv_stage_x(smem, in);
+    if constexpr (CMB)
+        gemv_stage_combine(smem + kGemvLdsHead, in);
+    else
+        gemv_stage_x(smem, in);
     __syncthreads();
 
     float acc[R];
@@ -383,10 +452,11 @@ inline int gemv_blocks(int units) {
     return b < kGemvMaxBlocks ? (b > 0 ? b : 1) : kGemvMaxBlocks;
 }
 
-template <typename WT, int R, int U, bool NT, class Epi>
+template <typename WT, int R, int U, bool NT, bool CMB = false, class Epi>
 hipError_t launch_gemv(const WT* W, const GemvIn& in, const Epi& epi, int units, hipStream_t s) {
-    hipLaunchKernelGGL((gemv_kernel<WT, R, U, NT, Epi>), dim3(gemv_blocks(units)), dim3(kGemvThreads),
-                       gemv_lds_bytes(in.cols), s, W, in, epi);
+    const size_t lds = gemv_lds_bytes(in.cols) + (CMB ? gemv_combine_lds(in) : 0);
+    hipLaunchKernelGGL((gemv_kernel<WT, R, U, NT, Epi, CMB>), dim3(gemv_blocks(units)), dim3(kGemvThreads), lds, s,
+                       W, in, epi);
     return hipGetLastError();
 }
 

@@ -6,6 +6,7 @@
 #include "attention.h"
 #include "common.h"
 #include "gemv.h"
+#include "ops_internal.h"
 #include "rope_table.h"
 
 namespace sli {
@@ -159,10 +160,12 @@ static int mha_ppw(int kv_dtype, int head_dim) {
     return kAttnNit * (64 / (head_dim / epv));
 }
 
+int attn_wg_positions(int kv_dtype, int head_dim) { return kAttnWaves * mha_ppw(kv_dtype, head_dim); }
+
 template <typename KT, int HD>
 static int mha_launch_hd(const float* q, const KT* kc, const KT* vc, float* out, int layer, int pos, const int32_t* pos_dev,
                          int T, int H, int Hkv, long long pos_stride, long long head_stride, long long layer_stride,
-                         float* part, hipStream_t s) {
+                         float* part, bool combine, hipStream_t s) {
     using Geo = AttnGeom<KT, HD>;
     constexpr int ppw_wg = kAttnWaves * Geo::PPW;
     const int wg_splits = (T + ppw_wg - 1) / ppw_wg;
@@ -179,6 +182,7 @@ static int mha_launch_hd(const float* q, const KT* kc, const KT* vc, float* out,
         default: return fail(SLI_ERR_SHAPE, "mha: heads per kv head must be 1, 2, 4 or 8");
     }
     SLI_HIP(hipGetLastError());
+    if (!combine) return SLI_OK;  // the consumer merges the partials itself (gemv_stage_combine)
     hipLaunchKernelGGL((attn_combine_kernel<HD>), dim3(H), dim3(128), 0, s, part, out, pos_dev, pos, wg_splits,
                        ppw_wg);
     SLI_HIP(hipGetLastError());
@@ -188,25 +192,25 @@ static int mha_launch_hd(const float* q, const KT* kc, const KT* vc, float* out,
 template <typename KT>
 int mha_launch(const float* q, const KT* kc, const KT* vc, float* out, int layer, int pos, const int32_t* pos_dev,
                int T, int hd, int H, int Hkv, long long pos_stride, long long head_stride, long long layer_stride,
-               float* part, hipStream_t s) {
+               float* part, hipStream_t s, bool combine) {
     if (hd == 128)
         return mha_launch_hd<KT, 128>(q, kc, vc, out, layer, pos, pos_dev, T, H, Hkv, pos_stride, head_stride,
-                                      layer_stride, part, s);
+                                      layer_stride, part, combine, s);
     if (hd == 64)
         return mha_launch_hd<KT, 64>(q, kc, vc, out, layer, pos, pos_dev, T, H, Hkv, pos_stride, head_stride,
-                                     layer_stride, part, s);
+                                     layer_stride, part, combine, s);
     return fail(SLI_ERR_SHAPE, "mha: head_dim must be 64 or 128");
 }
 
 template int mha_launch<float>(const float*, const float*, const float*, float*, int, int, const int32_t*, int, int,
-                               int, int, long long, long long, long long, float*, hipStream_t);
+                               int, int, long long, long long, long long, float*, hipStream_t, bool);
 template int mha_launch<__half>(const float*, const __half*, const __half*, float*, int, int, const int32_t*, int,
-                                int, int, int, long long, long long, long long, float*, hipStream_t);
+                                int, int, int, long long, long long, long long, float*, hipStream_t, bool);
 
 size_t mha_workspace_bytes(int T, int H, int hd) {
     const int ppw_wg_min = kAttnWaves * mha_ppw(SLI_DT_F32, hd);
     const size_t splits = (size_t)((T + ppw_wg_min - 1) / ppw_wg_min);
-    return sizeof(float) * (size_t)H * splits * (size_t)(hd + 2);
+    return sizeof(float) * (size_t)H * splits * (size_t)(hd + kAttnPartPad);
 }
 
 int embedding_launch(int token, const int32_t* token_dev, const void* table, int dtype, const float* row_scale,

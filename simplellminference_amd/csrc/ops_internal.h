@@ -7,9 +7,10 @@ namespace sli {
 template <typename KT>
 int mha_launch(const float* q, const KT* kc, const KT* vc, float* out, int layer, int pos, const int32_t* pos_dev,
                int T, int hd, int H, int Hkv, long long pos_stride, long long head_stride, long long layer_stride,
-               float* part, hipStream_t s);
+               float* part, hipStream_t s, bool combine = true);
 
 size_t mha_workspace_bytes(int T, int H, int hd);
+int attn_wg_positions(int kv_dtype, int head_dim);  // context positions per attention workgroup
 
 int embedding_launch(int token, const int32_t* token_dev, const void* table, int dtype, const float* row_scale,
                      float* out, int vocab, int dim, hipStream_t s);
