@@ -171,9 +171,6 @@ int sli_model_get_kv(sli_model* m, int32_t layer, int32_t which, int32_t upto, f
  * dequantised with its row scales). */
 int sli_model_get_weight(sli_model* m, int32_t kind, int32_t index, float* host, int64_t n);
 int sli_model_stream(sli_model* m, sli_stream_t* out);
-/* Diagnostic: with SLI_DEBUG_STAMPS=1 at create, workgroup 0's s_memrealtime (100 MHz) at the start,
- * barrier arrival and barrier exit of every persistent-step phase of the last step; returns the count. */
-int sli_model_debug_stamps(sli_model* m, unsigned long long* host, int32_t n);
 /* Algorithmic HBM bytes of one step on this rank (weights, KV at the current position) — SURVEY.md §8(d). */
 int sli_model_step_bytes(sli_model* m, double* weight_bytes, double* kv_bytes);
 /* Roofline probe: replays the step's weight-streaming (GEMV) kernels `iters` times between HIP events

@@ -87,7 +87,6 @@ _SIGS = {
     "sli_model_get_kv": (c_int, [c_vp, c_i32, c_i32, c_i32, c_vp]),
     "sli_model_get_weight": (c_int, [c_vp, c_i32, c_i32, c_vp, c_i64]),
     "sli_model_stream": (c_int, [c_vp, ctypes.POINTER(c_vp)]),
-    "sli_model_debug_stamps": (c_int, [c_vp, c_vp, c_i32]),
     "sli_model_step_bytes": (c_int, [c_vp, P_d, P_d]),
     "sli_model_time_gemv": (c_int, [c_vp, c_i32, P_d, P_d, P_i32]),
 }
@@ -123,7 +122,6 @@ def check(rc: int, where: str) -> None:
 
 def call(name: str, *args) -> int:
     rc = getattr(load(), name)(*args)
-    if isinstance(rc, int) and name not in ("sli_version", "sli_mha_workspace_bytes", "sli_comm_id_bytes",
-                                            "sli_model_debug_stamps"):
+    if isinstance(rc, int) and name not in ("sli_version", "sli_mha_workspace_bytes", "sli_comm_id_bytes"):
         check(rc, name)
     return rc

@@ -16,6 +16,34 @@
 
 namespace sli {
 
+// A byte range that extra workgroups of a latency-bound launch pull into the Infinity Cache (and L2)
+// for the NEXT launch, which then streams it at cache speed: decode attention reads 1/12 of a layer's
+// bytes and leaves HBM under-used, and the wo weights it precedes do not depend on it.
+struct StreamPrefetch {
+    const char* p = nullptr;
+    long long bytes = 0;
+    int blocks = 0;  // extra 256-thread workgroups appended to the grid
+};
+
+// Workgroup `b` of `pf.blocks` reads its contiguous share with default-policy (allocating) 16-byte loads.
+__device__ __forceinline__ void stream_prefetch_block(const StreamPrefetch& pf, int b) {
+    constexpr int U = 8;
+    const long long per = ((pf.bytes / pf.blocks) + 15) & ~15ll;
+    const long long lo = per * b, hi = min(pf.bytes, lo + per);
+    unsigned sink = 0;
+    for (long long o = lo + (long long)threadIdx.x * 16; o < hi; o += (long long)U * blockDim.x * 16) {
+        u32x4 w[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const long long a = min(o + (long long)j * blockDim.x * 16, hi - 16);
+            w[j] = *reinterpret_cast<const u32x4*>(pf.p + a);
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) sink ^= w[j].x;
+    }
+    if (sink == 0x9e3779b9u && pf.blocks < 0) asm volatile("" ::"v"(sink));  // keep the loads
+}
+
 template <typename KT>
 struct AttnArgs {
     const float* q;         // [hq * hd]
@@ -29,6 +57,7 @@ struct AttnArgs {
     int n_kv_heads;
     int max_splits;
     float scale;            // 1/sqrt(hd) (mha_kernel.cpp:41)
+    StreamPrefetch pf;      // optional: workgroups past n_kv_heads * max_splits prefetch this range
 };
 
 constexpr int kAttnNit = 16;  // 16-byte vectors per lane per operand per wave (K and V each)
@@ -54,6 +83,10 @@ __global__ void __launch_bounds__(256) attn_partial_kernel(AttnArgs<KT> a) {
     __shared__ float sh[kAttnWaves][G][HD + 2];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
+    if ((int)blockIdx.x >= a.n_kv_heads * a.max_splits) {
+        stream_prefetch_block(a.pf, (int)blockIdx.x - a.n_kv_heads * a.max_splits);
+        return;
+    }
     const int kvh = blockIdx.x / a.max_splits;  // max_splits counts workgroup splits here
     const int wgs = blockIdx.x - kvh * a.max_splits;
     const int pos = a.pos_dev ? *a.pos_dev : a.pos_host;

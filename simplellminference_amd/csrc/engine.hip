@@ -28,9 +28,8 @@
 #include "common.h"
 #include "gemv.h"
 #include "ops_internal.h"
-#include "persistent.h"
-#include "persistent_launch.h"
 #include "rope_table.h"
+#include "step_state.h"
 
 namespace sli {
 
@@ -53,6 +52,7 @@ struct sli_model {
     ncclComm_t comm = nullptr;
     bool partial = false;    // wo/down write per-rank partials (+ residual on rank 0) into xpart
     bool collectives = false;  // all-reduce partials / argmax keys over RCCL inside the step
+    int pf_attn_blocks = 0;    // extra attention workgroups that pull the layer's wo weights into the caches
     // local (this rank's) geometry
     int D = 0, L = 0, T = 0, V = 0, hd = 0, hq = 0, hkv = 0, Il = 0;
     int v_lo = 0, v_n = 0;
@@ -71,14 +71,6 @@ struct sli_model {
     sli::DevState* st = nullptr;
     int32_t* prompt = nullptr;
     int32_t* hist = nullptr;
-    // persistent step (persistent.h)
-    bool persistent = false;
-    int grid = 256;                          // one 1024-thread workgroup per CU
-    size_t step_lds = 0;
-    sli::StepParams* dparams = nullptr;      // device copy of the step parameters
-    sli::LayerPtrs* dlayers = nullptr;
-    unsigned* bar = nullptr;                 // grid-barrier words, zeroed before every launch
-    unsigned long long* stamps = nullptr;    // SLI_DEBUG_STAMPS: per-phase s_memrealtime (100 MHz)
     hipGraph_t graph = nullptr;
     hipGraphExec_t graph_exec = nullptr;
     std::vector<void*> allocs;
@@ -286,7 +278,7 @@ struct StepRecorder {
         KT* kc = (KT*)m->kc + (size_t)l * m->hkv * m->T * m->hd;
         KT* vc = (KT*)m->vc + (size_t)l * m->hkv * m->T * m->hd;
         EpiQKV<KT> e{m->q, kc, vc, w.qkv_s, &m->st->pos, m->sin_t, m->cos_t, m->hq, m->hkv, m->hd, m->T};
-        SLI_HIP((launch_gemv<WT, 2, 8, NT>((const WT*)w.qkv, in, e, (m->hq + 2 * m->hkv) * (m->hd / 2), m->stream)));
+        SLI_HIP((launch_gemv<WT, 2, 4, NT, false, false>((const WT*)w.qkv, in, e, (m->hq + 2 * m->hkv) * (m->hd / 2), m->stream)));
         return SLI_OK;
     }
     static bool fused_combine_fits(const sli_model* m) {
@@ -306,26 +298,26 @@ struct StepRecorder {
             in.ppw_wg = ppw;
             in.max_splits = (m->T + ppw - 1) / ppw;
         }
-        EpiStore<2> e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, w.wo_s, 1.0f, m->D};
+        EpiStore<1> e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, w.wo_s, 1.0f, m->D};
         if (fused_combine)
-            SLI_HIP((launch_gemv<WT, 2, 8, NT, true>((const WT*)w.wo, in, e, (m->D + 1) / 2, m->stream)));
+            SLI_HIP((launch_gemv<WT, 1, 4, NT, true, true>((const WT*)w.wo, in, e, m->D, m->stream)));
         else
-            SLI_HIP((launch_gemv<WT, 2, 8, NT>((const WT*)w.wo, in, e, (m->D + 1) / 2, m->stream)));
+            SLI_HIP((launch_gemv<WT, 1, 4, NT, false, true>((const WT*)w.wo, in, e, m->D, m->stream)));
         return SLI_OK;
     }
     static int gemv_gu(sli_model* m, int l) {
         const LayerW& w = m->layers[l];
         GemvIn in{m->x, m->norms + (size_t)(2 * l + 1) * m->D, m->c.eps, m->D};
         EpiSwiGLU e{m->act, w.gu_s, m->Il, m->c.act_mode};
-        SLI_HIP((launch_gemv<WT, 2, 8, NT>((const WT*)w.gu, in, e, m->Il, m->stream)));
+        SLI_HIP((launch_gemv<WT, 2, 4, NT, false, false>((const WT*)w.gu, in, e, m->Il, m->stream)));
         return SLI_OK;
     }
     static int gemv_down(sli_model* m, int l) {
         const LayerW& w = m->layers[l];
         const bool tp = m->partial;
         GemvIn in{m->act, nullptr, 0.0f, m->Il};
-        EpiStore<2> e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, w.down_s, 1.0f, m->D};
-        SLI_HIP((launch_gemv<WT, 2, 8, NT>((const WT*)w.down, in, e, (m->D + 1) / 2, m->stream)));
+        EpiStore<1> e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, w.down_s, 1.0f, m->D};
+        SLI_HIP((launch_gemv<WT, 1, 8, NT, false, true>((const WT*)w.down, in, e, m->D, m->stream)));
         return SLI_OK;
     }
     static int lm_head_blocks(sli_model* m) { return gemv_blocks((m->v_n + 1) / 2); }
@@ -333,7 +325,7 @@ struct StepRecorder {
         GemvIn in{m->x, m->norms + (size_t)(2 * m->L) * m->D, m->c.eps, m->D};
         EpiLogits<2> e{m->logits, m->keys, m->emb_s ? m->emb_s + m->v_lo : nullptr, m->v_n, m->v_lo, 0ull};
         const WT* w = (const WT*)m->emb + (size_t)m->v_lo * m->D;
-        SLI_HIP((launch_gemv<WT, 2, 8, NT>(w, in, e, (m->v_n + 1) / 2, m->stream)));
+        SLI_HIP((launch_gemv<WT, 2, 4, NT, false, false>(w, in, e, (m->v_n + 1) / 2, m->stream)));
         return SLI_OK;
     }
     static int allreduce_x(sli_model* m) {
@@ -343,44 +335,19 @@ struct StepRecorder {
             SLI_HIP(hipMemcpyAsync(m->x, m->xpart, sizeof(float) * m->D, hipMemcpyDeviceToDevice, m->stream));
         return SLI_OK;
     }
-    // ---- persistent step (persistent.h): instantiated for the common storage pairs and head shapes
-    static bool persistent_ok(const sli_model* m) {
-        return persistent_supported(m->c.w_dtype, m->c.kv_dtype, m->hd, m->hq / m->hkv);
-    }
-    static int persist(sli_model* m, int pb, int pe, int fin) {
-        return persistent_launch(m->c.w_dtype, m->c.kv_dtype, m->hd, m->hq / m->hkv, m->dparams, m->grid,
-                                 m->step_lds, m->bar, pb, pe, fin, m->stream);
-    }
-    static int record_persistent(sli_model* m) {
-        const int last = m->L * kPhasesPerLayer;
-        if (!m->partial) return persist(m, 0, last + 1, 1);  // the whole step is one launch
-        for (int l = 0; l < m->L; ++l) {                     // TP: cut at the two all-reduces per layer
-            SLI_TRY(persist(m, l * kPhasesPerLayer, l * kPhasesPerLayer + kPhGU, 0));
-            SLI_TRY(allreduce_x(m));
-            SLI_TRY(persist(m, l * kPhasesPerLayer + kPhGU, (l + 1) * kPhasesPerLayer, 0));
-            SLI_TRY(allreduce_x(m));
-        }
-        SLI_TRY(persist(m, last, last + 1, 0));
-        hipStream_t s = m->stream;
-        hipLaunchKernelGGL(keyreduce_kernel, dim3(1), dim3(256), 0, s, m->keys, m->grid, m->st);
-        SLI_HIP(hipGetLastError());
-        if (m->collectives) SLI_NCCL(ncclAllReduce(&m->st->key, &m->st->key, 1, ncclUint64, ncclMax, m->comm, s));
-        hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1), 0, s, m->st, m->prompt, m->hist, m->T);
-        SLI_HIP(hipGetLastError());
-        return SLI_OK;
-    }
-    static int uses_persistent(sli_model* m) { return m->persistent && persistent_ok(m) ? 1 : 0; }
-
     static int record(sli_model* m) {
-        if (m->persistent && persistent_ok(m)) return record_persistent(m);
         hipStream_t s = m->stream;
         SLI_TRY(embedding_launch(0, &m->st->token, m->emb, m->c.w_dtype, m->emb_s, m->x, m->V, m->D, s));
         const long long ps = m->hd, hs = (long long)m->T * m->hd, ls = (long long)m->hkv * m->T * m->hd;
         const bool fuse = fused_combine_fits(m);  // split merge inside the wo GEMV prologue
         for (int l = 0; l < m->L; ++l) {
             SLI_TRY(gemv_qkv(m, l));
+            StreamPrefetch pf;
+            pf.p = (const char*)m->layers[l].wo;
+            pf.bytes = (long long)m->D * m->hq * m->hd * (long long)m->wbytes;
+            pf.blocks = m->pf_attn_blocks;
             SLI_TRY(mha_launch<KT>(m->q, (const KT*)m->kc, (const KT*)m->vc, m->attn, l, 0, &m->st->pos, m->T, m->hd,
-                                   m->hq, m->hkv, ps, hs, ls, m->part, s, /*combine=*/!fuse));
+                                   m->hq, m->hkv, ps, hs, ls, m->part, s, /*combine=*/!fuse, pf));
             SLI_TRY(gemv_wo(m, l, fuse));
             SLI_TRY(allreduce_x(m));
             SLI_TRY(gemv_gu(m, l));
@@ -570,12 +537,7 @@ int sli_model_create(const sli_model_config* cfg, const void* comm_id, sli_model
     A((void**)&m->attn, sizeof(float) * m->hq * hd);
     A((void**)&m->act, sizeof(float) * m->Il);
     A((void**)&m->logits, sizeof(float) * m->v_n);
-    {  // split-context partials [hq][splits][hd + kAttnPartPad] (launch and persistent paths)
-        const int ppw_wg_f32 = pattn_ppw_wg(hd, 4, 4);  // smallest persistent slice (f32 KV, GQA-4)
-        const size_t persist_bytes =
-            sizeof(float) * (size_t)m->hq * ((m->T + ppw_wg_f32 - 1) / ppw_wg_f32) * (hd + kPartStride);
-        A((void**)&m->part, std::max(mha_workspace_bytes(m->T, m->hq, hd), persist_bytes));
-    }
+    A((void**)&m->part, mha_workspace_bytes(m->T, m->hq, hd));  // split-context partials
     A((void**)&m->sin_t, sizeof(float) * (size_t)m->T * (hd / 2));
     A((void**)&m->cos_t, sizeof(float) * (size_t)m->T * (hd / 2));
     A((void**)&m->keys, sizeof(unsigned long long) * kGemvMaxBlocks);
@@ -601,51 +563,9 @@ int sli_model_create(const sli_model_config* cfg, const void* comm_id, sli_model
     const bool no_comm = c.tp_size > 1 && std::getenv("SLI_DEBUG_NOCOMM") != nullptr;
     m->partial = c.tp_size > 1 || force_comm;
     m->collectives = (c.tp_size > 1 && !no_comm) || force_comm;
-
-    // persistent-step parameters (persistent.h)
-    {
-        // Default: one launch per fused op (measured faster); SLI_STEP_MODE=persistent runs the
-        // whole step as one persistent launch with grid barriers (persistent.h, experimental).
-        const char* mode = std::getenv("SLI_STEP_MODE");
-        m->persistent = mode && std::string(mode) == "persistent";
-        int cus = 0;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device) != hipSuccess || cus <= 0)
-            cus = kGemvCUs;
-        m->grid = std::min(cus, kGemvMaxBlocks);
-        const int g = m->hq / m->hkv;
-        const size_t xs_floats = (size_t)kGemvLdsHead + std::max(std::max(m->D, m->Il), m->hq * hd);
-        const size_t attn_floats = (size_t)4 * kAttnWaves * g * (hd + 2);
-        m->step_lds = sizeof(float) * std::max(xs_floats, attn_floats);
-        std::vector<LayerPtrs> lp(m->L);
-        for (int l = 0; l < m->L; ++l) {
-            const LayerW& w = m->layers[l];
-            lp[l] = LayerPtrs{w.qkv, w.qkv_s, w.wo, w.wo_s, w.gu, w.gu_s, w.down, w.down_s};
-        }
-        A((void**)&m->dlayers, sizeof(LayerPtrs) * m->L);
-        A((void**)&m->dparams, sizeof(StepParams));
-        A((void**)&m->bar, sizeof(unsigned) * kBarWords);
-        unsigned long long* stamps = nullptr;
-        if (std::getenv("SLI_DEBUG_STAMPS")) A((void**)&stamps, sizeof(unsigned long long) * 3 * (m->L * kPhasesPerLayer + 1));
-        if (rc != SLI_OK) return bail(rc);
-        const int ppw_wg = pattn_ppw_wg(hd, c.kv_dtype == SLI_DT_F16 ? 2 : 4, g);
-        StepParams P{};
-        P.D = m->D; P.L = m->L; P.T = m->T; P.hd = hd; P.hq = m->hq; P.hkv = m->hkv; P.Il = m->Il;
-        P.v_lo = m->v_lo; P.v_n = m->v_n; P.V = m->V;
-        P.silu = c.act_mode; P.partial = m->partial ? 1 : 0; P.rank = c.tp_rank; P.eps = c.eps;
-        P.emb = m->emb; P.emb_s = m->emb_s; P.norms = m->norms; P.layers = m->dlayers;
-        P.kc = m->kc; P.vc = m->vc;
-        P.x = m->x; P.xpart = m->xpart; P.q = m->q; P.act = m->act; P.logits = m->logits; P.part = m->part;
-        P.sin_t = m->sin_t; P.cos_t = m->cos_t; P.keys = m->keys; P.st = m->st; P.prompt = m->prompt;
-        P.hist = m->hist; P.bar = m->bar;
-        P.attn_splits = (m->T + ppw_wg - 1) / ppw_wg;
-        P.stamps = stamps;
-        const char* dbg = std::getenv("SLI_DEBUG_BARRIER");
-        P.debug_flags = dbg ? std::atoi(dbg) : 0;
-        m->stamps = stamps;
-        if (hipMemcpy(m->dlayers, lp.data(), sizeof(LayerPtrs) * m->L, hipMemcpyHostToDevice) != hipSuccess ||
-            hipMemcpy(m->dparams, &P, sizeof(StepParams), hipMemcpyHostToDevice) != hipSuccess ||
-            hipMemset(m->bar, 0, sizeof(unsigned) * kBarWords) != hipSuccess)
-            return bail(fail(SLI_ERR_HIP, "persistent step parameters upload"));
+    {  // attention-side prefetch of the wo weights (workgroups appended to the attention grid)
+        const char* pf = std::getenv("SLI_PF_ATTN");
+        m->pf_attn_blocks = pf ? std::atoi(pf) : 0;
     }
 
     if (m->collectives) {
@@ -899,15 +819,6 @@ int sli_model_get_weight(sli_model* m, int32_t kind, int32_t index, float* host,
     return SLI_OK;
 }
 
-int sli_model_debug_stamps(sli_model* m, unsigned long long* host, int32_t n) {
-    SLI_CHECK(m && host, SLI_ERR_ARG, "null argument");
-    SLI_CHECK(m->stamps, SLI_ERR_STATE, "model created without SLI_DEBUG_STAMPS=1");
-    const int32_t have = 3 * (m->L * kPhasesPerLayer + 1);
-    SLI_CHECK(n >= have, SLI_ERR_SHAPE, "host buffer too small");
-    SLI_HIP(hipStreamSynchronize(m->stream));
-    SLI_HIP(hipMemcpy(host, m->stamps, sizeof(unsigned long long) * have, hipMemcpyDeviceToHost));
-    return have;
-}
 
 int sli_model_stream(sli_model* m, sli_stream_t* out) {
     SLI_CHECK(m && out, SLI_ERR_ARG, "null argument");

@@ -11,6 +11,8 @@
 //     (plain store, residual add, RoPE + KV-cache write, SwiGLU, logits + argmax keys).
 // Grid-stride over units so a launch is sized to the chip, not to the matrix.
 #pragma once
+#include <type_traits>
+
 #include "common.h"
 
 namespace sli {
@@ -34,124 +36,147 @@ inline size_t gemv_lds_bytes(int cols) { return sizeof(float) * (size_t)(kGemvLd
 
 constexpr int kGemvStageV4 = 4;  // float4 of x per thread: 1024 threads x 4 x 4 = 16384 columns
 
-// Stage x (optionally RMS-normalised) into LDS in ONE round trip: every thread issues all of its float4
-// loads of x (and of the norm weight) before using any (clamped indices, no branch around a load).
-// All LDS lives in one dynamic array (G17: no static __shared__ in front of the dynamic region, so the
-// b128 reads stay 16-byte aligned). Requires cols % 4 == 0 and 16-byte aligned x / norm_w.
-// Merge the attention partials straight into the staged x (replaces attn_combine_kernel and its launch).
-// The (m, l) pairs of every live split go through LDS once per workgroup; each thread then merges the
-// o rows of its 4 columns, CH splits per batch of loads, with the combine kernel's exact arithmetic:
-// M = max m_i, w_i = e^{m_i - M}, x = (sum_i w_i o_i) / (sum_i w_i l_i), summed in split order.
-// The first batch of o loads is issued before the (m, l) round trip so the two overlap.
-// LDS: the staged x [cols] is followed by the (m, l) table [cols / hd][live splits] (gemv_combine_lds).
-__device__ __forceinline__ void gemv_stage_combine(float* xs, const GemvIn& in) {
-    constexpr int CH = 8;
-    const int tid = threadIdx.x, nt = blockDim.x;
-    const int ps = in.hd + kAttnPartPad;
-    const int ns = min(*in.pos / in.ppw_wg + 1, in.max_splits);
-    const int n4 = in.cols >> 2;
-    const int nml = (in.cols / in.hd) * ns;
-    float2* mls = reinterpret_cast<float2*>(xs + in.cols);
-    const float* part = in.part;
-    auto row = [&](int h, int i) { return part + ((size_t)h * in.max_splits + i) * ps; };
-
-    float4 po[CH];
-    const int h0 = (tid << 2) / in.hd, d0 = (tid << 2) - h0 * in.hd;
-    if (tid < n4) {
+// The prologue is split into issue (global loads into registers) and commit (normalise, write LDS) so
+// the kernel can issue its input loads FIRST, its weight loads second, and wait only for the input:
+// s_waitcnt vmcnt counts in issue order, so an input load issued after the weights would wait for the
+// whole first weight chunk (measured: x staged 6-11 us into a 10-30 us launch), and no wave could
+// start consuming weights until every wave's first chunk had landed.
+struct XStage {
+    float4 xr[kGemvStageV4];
+    float4 wr[kGemvStageV4];
+    __device__ __forceinline__ void issue(const GemvIn& in) {
+        const int tid = threadIdx.x, nt = blockDim.x, n4 = in.cols >> 2;
+        const float4* x4 = reinterpret_cast<const float4*>(in.x);
 #pragma unroll
-        for (int j = 0; j < CH; ++j) po[j] = *reinterpret_cast<const float4*>(row(h0, min(j, ns - 1)) + d0);
+        for (int k = 0; k < kGemvStageV4; ++k)  // k * nt < n4 is uniform; the clamp covers the ragged tail
+            if (k * nt < n4) xr[k] = x4[min(tid + k * nt, n4 - 1)];
+        if (in.norm_w != nullptr) {
+            const float4* w4 = reinterpret_cast<const float4*>(in.norm_w);
+#pragma unroll
+            for (int k = 0; k < kGemvStageV4; ++k)
+                if (k * nt < n4) wr[k] = w4[min(tid + k * nt, n4 - 1)];
+        }
     }
-    for (int k = tid; k < nml; k += nt) {
-        const int h = k / ns, i = k - h * ns;
-        mls[k] = *reinterpret_cast<const float2*>(row(h, i) + in.hd);
-    }
-    __syncthreads();
-    for (int c4 = tid; c4 < n4; c4 += nt) {
-        const int h = (c4 << 2) / in.hd, d = (c4 << 2) - h * in.hd;
-        const float2* ml = mls + h * ns;
-        float M = -INFINITY;
-        for (int i = 0; i < ns; ++i) M = fmaxf(M, ml[i].x);
-        float L = 0.0f;
-        float4 o = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        for (int i0 = 0; i0 < ns; i0 += CH) {
-            if (c4 != tid || i0 != 0) {
+    // x (optionally RMS-normalised, rms_kernel.cpp:5-23) into LDS; the caller then barriers.
+    __device__ __forceinline__ void commit(float* smem, const GemvIn& in) {
+        float* red = smem;
+        float* xs = smem + kGemvLdsHead;
+        const int tid = threadIdx.x, nt = blockDim.x, n4 = in.cols >> 2;
+        if (in.norm_w == nullptr) {
 #pragma unroll
-                for (int j = 0; j < CH; ++j) po[j] = *reinterpret_cast<const float4*>(row(h, min(i0 + j, ns - 1)) + d);
-            }
+            for (int k = 0; k < kGemvStageV4; ++k)
+                if (tid + k * nt < n4) reinterpret_cast<float4*>(xs)[tid + k * nt] = xr[k];
+            return;
+        }
+        float ss = 0.0f;
 #pragma unroll
-            for (int j = 0; j < CH; ++j) {
-                if (i0 + j < ns) {
-                    const float w = expf(ml[i0 + j].x - M);
-                    o.x = fmaf(w, po[j].x, o.x);
-                    o.y = fmaf(w, po[j].y, o.y);
-                    o.z = fmaf(w, po[j].z, o.z);
-                    o.w = fmaf(w, po[j].w, o.w);
-                    L = fmaf(w, ml[i0 + j].y, L);
-                }
+        for (int k = 0; k < kGemvStageV4; ++k) {
+            if (tid + k * nt < n4) {
+                ss += xr[k].x * xr[k].x;
+                ss += xr[k].y * xr[k].y;
+                ss += xr[k].z * xr[k].z;
+                ss += xr[k].w * xr[k].w;
             }
         }
-        reinterpret_cast<float4*>(xs)[c4] = make_float4(o.x / L, o.y / L, o.z / L, o.w / L);
+        ss = wave_sum(ss);
+        if ((tid & 63) == 0) red[tid >> 6] = ss;
+        __syncthreads();
+        if (tid == 0) {
+            float t = 0.0f;
+            for (int w = 0; w < (nt >> 6); ++w) t += red[w];
+            const float tep = t / (float)in.cols;  // rms_kernel.cpp:17
+            const float rms = sqrtf(tep + in.eps);  // :18
+            red[32] = 1.0f / rms;                   // :19
+        }
+        __syncthreads();
+        const float inv = red[32];
+#pragma unroll
+        for (int k = 0; k < kGemvStageV4; ++k) {
+            if (tid + k * nt < n4) {  // :20-22  y = (x * inv) * w
+                float4 o;
+                o.x = (xr[k].x * inv) * wr[k].x;
+                o.y = (xr[k].y * inv) * wr[k].y;
+                o.z = (xr[k].z * inv) * wr[k].z;
+                o.w = (xr[k].w * inv) * wr[k].w;
+                reinterpret_cast<float4*>(xs)[tid + k * nt] = o;
+            }
+        }
     }
-}
+};
+
+// Merge the attention partials straight into the staged x (replaces attn_combine_kernel and its launch):
+// x[h*hd + d] = sum_i e^{m_i - M} o_i[d] / sum_i e^{m_i - M} l_i over the live splits of head h, summed in
+// split order. issue(): this thread's first CH o rows and its first (m, l) pair; commit(): the (m, l)
+// table through LDS, then the merge (further o batches, when a head has more than CH splits, are loaded
+// there and queue behind the weights). LDS: staged x [cols], then the (m, l) table (gemv_combine_lds).
+struct CombineStage {
+    static constexpr int CH = 8;
+    float4 po[CH];
+    float2 ml0;
+    __device__ __forceinline__ static const float* row(const GemvIn& in, int h, int i) {
+        return in.part + ((size_t)h * in.max_splits + i) * (in.hd + kAttnPartPad);
+    }
+    __device__ __forceinline__ static int live(const GemvIn& in) { return min(*in.pos / in.ppw_wg + 1, in.max_splits); }
+    __device__ __forceinline__ void issue(const GemvIn& in) {
+        const int tid = threadIdx.x, ns = live(in);
+        const int n4 = in.cols >> 2, nml = (in.cols / in.hd) * ns;
+        const int c4 = min(tid, n4 - 1);
+        const int h0 = (c4 << 2) / in.hd, d0 = (c4 << 2) - h0 * in.hd;
+#pragma unroll
+        for (int j = 0; j < CH; ++j) po[j] = *reinterpret_cast<const float4*>(row(in, h0, min(j, ns - 1)) + d0);
+        const int k = min(tid, nml - 1), h = k / ns, i = k - h * ns;
+        ml0 = *reinterpret_cast<const float2*>(row(in, h, i) + in.hd);
+    }
+    __device__ __forceinline__ void commit(float* smem, const GemvIn& in) {
+        float* xs = smem + kGemvLdsHead;
+        const int tid = threadIdx.x, nt = blockDim.x, ns = live(in);
+        const int n4 = in.cols >> 2, nml = (in.cols / in.hd) * ns;
+        float2* mls = reinterpret_cast<float2*>(xs + in.cols);
+        if (tid < nml) mls[tid] = ml0;
+        for (int k = tid + nt; k < nml; k += nt) {
+            const int h = k / ns, i = k - h * ns;
+            mls[k] = *reinterpret_cast<const float2*>(row(in, h, i) + in.hd);
+        }
+        __syncthreads();
+        for (int c4 = tid; c4 < n4; c4 += nt) {
+            const int h = (c4 << 2) / in.hd, d = (c4 << 2) - h * in.hd;
+            const float2* ml = mls + h * ns;
+            float M = -INFINITY;
+            for (int i = 0; i < ns; ++i) M = fmaxf(M, ml[i].x);
+            float L = 0.0f;
+            float4 o = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            for (int i0 = 0; i0 < ns; i0 += CH) {
+                if (c4 != tid || i0 != 0) {
+#pragma unroll
+                    for (int j = 0; j < CH; ++j)
+                        po[j] = *reinterpret_cast<const float4*>(row(in, h, min(i0 + j, ns - 1)) + d);
+                }
+#pragma unroll
+                for (int j = 0; j < CH; ++j) {
+                    if (i0 + j < ns) {
+                        const float w = expf(ml[i0 + j].x - M);
+                        o.x = fmaf(w, po[j].x, o.x);
+                        o.y = fmaf(w, po[j].y, o.y);
+                        o.z = fmaf(w, po[j].z, o.z);
+                        o.w = fmaf(w, po[j].w, o.w);
+                        L = fmaf(w, ml[i0 + j].y, L);
+                    }
+                }
+            }
+            reinterpret_cast<float4*>(xs)[c4] = make_float4(o.x / L, o.y / L, o.z / L, o.w / L);
+        }
+    }
+};
 
 inline size_t gemv_combine_lds(const GemvIn& in) {
     return sizeof(float2) * (size_t)(in.cols / in.hd) * in.max_splits;
 }
 
+// One-shot staging for callers that have nothing to overlap it with.
 __device__ __forceinline__ void gemv_stage_x(float* smem, const GemvIn& in) {
-    float* red = smem;
-    float* xs = smem + kGemvLdsHead;
-    const int tid = threadIdx.x;
-    const int nt = blockDim.x;
-    const int n4 = in.cols >> 2;
-    const float4* x4 = reinterpret_cast<const float4*>(in.x);
-    float4 xr[kGemvStageV4];
-#pragma unroll
-    for (int k = 0; k < kGemvStageV4; ++k) xr[k] = x4[min(tid + k * nt, n4 - 1)];
-    if (in.norm_w == nullptr) {
-#pragma unroll
-        for (int k = 0; k < kGemvStageV4; ++k)
-            if (tid + k * nt < n4) reinterpret_cast<float4*>(xs)[tid + k * nt] = xr[k];
-        return;
-    }
-    const float4* w4 = reinterpret_cast<const float4*>(in.norm_w);
-    float4 wr[kGemvStageV4];
-#pragma unroll
-    for (int k = 0; k < kGemvStageV4; ++k) wr[k] = w4[min(tid + k * nt, n4 - 1)];
-    float ss = 0.0f;
-#pragma unroll
-    for (int k = 0; k < kGemvStageV4; ++k) {
-        if (tid + k * nt < n4) {
-            ss += xr[k].x * xr[k].x;
-            ss += xr[k].y * xr[k].y;
-            ss += xr[k].z * xr[k].z;
-            ss += xr[k].w * xr[k].w;
-        }
-    }
-    ss = wave_sum(ss);
-    const int wave = tid >> 6;
-    if ((tid & 63) == 0) red[wave] = ss;
-    __syncthreads();
-    if (tid == 0) {
-        float t = 0.0f;
-        for (int w = 0; w < (nt >> 6); ++w) t += red[w];
-        const float tep = t / (float)in.cols;  // rms_kernel.cpp:17
-        const float rms = sqrtf(tep + in.eps);  // :18
-        red[32] = 1.0f / rms;                   // :19
-    }
-    __syncthreads();
-    const float inv = red[32];
-#pragma unroll
-    for (int k = 0; k < kGemvStageV4; ++k) {
-        if (tid + k * nt < n4) {  // :20-22  y = (x * inv) * w
-            float4 o;
-            o.x = (xr[k].x * inv) * wr[k].x;
-            o.y = (xr[k].y * inv) * wr[k].y;
-            o.z = (xr[k].z * inv) * wr[k].z;
-            o.w = (xr[k].w * inv) * wr[k].w;
-            reinterpret_cast<float4*>(xs)[tid + k * nt] = o;
-        }
-    }
+    XStage st;
+    st.issue(in);
+    st.commit(smem, in);
 }
 
 // acc[r] += sum over the U vectors (64 lanes apart, starting at vector index v) of W[r] . x.
@@ -184,84 +209,92 @@ __device__ __forceinline__ void gemv_chunk(const u32x4 (&w)[U][R], const float* 
     }
 }
 
-// Balanced static schedule: wave gw of W owns units [gw*N/W, (gw+1)*N/W) (sizes differ by at most one),
-// so no wave is left with a second pass while the rest of the chip idles. The first weight chunk of the
-// wave's first unit is issued BEFORE the x-staging prologue, so the prologue's L2 round trips and
-// barriers overlap the first HBM round trip instead of preceding it.
-// CMB: stage x by merging attention partials (gemv_stage_combine) instead of reading in.x.
-template <typename WT, int R, int U, bool NT, class Epi, bool CMB = false>
+// Wave-level schedule. Wave gw of the grid owns units [gw*N/W, (gw+1)*N/W) (balanced: sizes differ by at
+// most one); a unit is R rows chosen by the epilogue, streamed in chunks of U 16-byte vectors per row
+// per lane. The wave's work is the flat sequence of (unit, chunk) steps; with DB the next step's loads
+// are issued before the current step is consumed (two register buffers), so each wave keeps a chunk in
+// flight while it computes and waves drift apart instead of stalling together at chunk boundaries.
+// Prologue order: input loads, first weight chunk, input commit + barrier (see XStage).
+// CMB: stage x by merging attention partials (CombineStage) instead of reading in.x.
+template <typename WT, int R, int U, bool NT, class Epi, bool CMB = false, bool DB = (R * U <= 8)>
 __global__ void __launch_bounds__(kGemvThreads) gemv_kernel(const WT* __restrict__ W, GemvIn in, Epi epi_in) {
     Epi epi = epi_in;  // mutable per-thread copy (EpiLogits keeps a running key)
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const float* xs = smem + kGemvLdsHead;
 
     constexpr int EPV = Vec16<WT>::N;
+    constexpr int CV = U * 64;  // vectors per row per chunk
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int nwaves = blockDim.x >> 6;
-    const int cols = in.cols;
-    const int nvec = cols / EPV;
-    const size_t row_bytes = (size_t)cols * sizeof(WT);
+    const int nvec = in.cols / EPV;
+    const size_t row_bytes = (size_t)in.cols * sizeof(WT);
     const int nunits = epi.units();
     const long long gw = (long long)blockIdx.x * nwaves + wave;
     const long long nw = (long long)gridDim.x * nwaves;
     const int u_begin = (int)(gw * nunits / nw);
     const int u_end = (int)((gw + 1) * nunits / nw);
+    const int cpr = (nvec + CV - 1) / CV;  // chunks per row
+    const int nsteps = (u_end - u_begin) * cpr;
 
-    // prefetch: first U-chunk of the first unit (full chunk only when it lies inside the row)
-    const bool have_pre = u_begin < u_end && lane + (U - 1) * 64 < nvec;
-    u32x4 pre[U][R];
-    if (have_pre) {
+    using Stage = typename std::conditional<CMB, CombineStage, XStage>::type;
+    Stage stage;
+    stage.issue(in);
+
+    auto load_step = [&](int k, u32x4 (&w)[U][R]) {
+        const int u = u_begin + k / cpr;
+        const int v = (k % cpr) * CV + lane;
         int rows[R];
-        epi.rows(u_begin, rows);
+        epi.rows(u, rows);
 #pragma unroll
-        for (int j = 0; j < U; ++j)
+        for (int j = 0; j < U; ++j) {
+            const int vj = min(v + j * 64, nvec - 1);  // clamp, never branch around a load
 #pragma unroll
             for (int r = 0; r < R; ++r)
-                pre[j][r] = load16<NT>(reinterpret_cast<const char*>(W) + (size_t)rows[r] * row_bytes +
-                                       (size_t)(lane + j * 64) * 16);
-    }
-    if constexpr (CMB)
-        gemv_stage_combine(smem + kGemvLdsHead, in);
-    else
-        gemv_stage_x(smem, in);
-    __syncthreads();
-
+                w[j][r] = load16<NT>(reinterpret_cast<const char*>(W) + (size_t)rows[r] * row_bytes + (size_t)vj * 16);
+        }
+    };
     float acc[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = 0.0f;
-    if (have_pre) gemv_chunk<WT, R, U>(pre, xs, lane, acc);  // peeled: pre dies here
-
-    for (int u = u_begin; u < u_end; ++u) {
-        int rows[R];
-        epi.rows(u, rows);
-        const char* wp[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) wp[r] = reinterpret_cast<const char*>(W) + (size_t)rows[r] * row_bytes;
-        int v = (u == u_begin && have_pre) ? lane + U * 64 : lane;
-        for (; v + (U - 1) * 64 < nvec; v += U * 64) {
-            u32x4 w[U][R];
-#pragma unroll
-            for (int j = 0; j < U; ++j)
-#pragma unroll
-                for (int r = 0; r < R; ++r) w[j][r] = load16<NT>(wp[r] + (size_t)(v + j * 64) * 16);
+    auto consume_step = [&](int k, const u32x4(&w)[U][R]) {
+        const int c = k % cpr;
+        const int v = c * CV + lane;
+        if ((c + 1) * CV <= nvec)
             gemv_chunk<WT, R, U>(w, xs, v, acc);
-        }
-        if (v < nvec) {  // remainder (< U*64 vectors): one masked chunk, all loads in flight together
-            u32x4 w[U][R];
-#pragma unroll
-            for (int j = 0; j < U; ++j) {
-                const int vj = min(v + j * 64, nvec - 1);  // clamp, never branch around a load
-#pragma unroll
-                for (int r = 0; r < R; ++r) w[j][r] = load16<NT>(wp[r] + (size_t)vj * 16);
-            }
+        else
             gemv_chunk<WT, R, U, true>(w, xs, v, acc, nvec);
+        if (c == cpr - 1) {  // unit complete
+            const int u = u_begin + k / cpr;
+            int rows[R];
+            epi.rows(u, rows);
+#pragma unroll
+            for (int r = 0; r < R; ++r) acc[r] = wave_sum(acc[r]);
+            epi.store(u, rows, acc, lane);
+#pragma unroll
+            for (int r = 0; r < R; ++r) acc[r] = 0.0f;
         }
-#pragma unroll
-        for (int r = 0; r < R; ++r) acc[r] = wave_sum(acc[r]);
-        epi.store(u, rows, acc, lane);
-#pragma unroll
-        for (int r = 0; r < R; ++r) acc[r] = 0.0f;
+    };
+
+    u32x4 wa[U][R];
+    if (nsteps > 0) load_step(0, wa);
+    stage.commit(smem, in);
+    __syncthreads();
+    if constexpr (DB) {
+        u32x4 wb[U][R];
+        int k = 0;
+        for (; k + 1 < nsteps; k += 2) {
+            load_step(k + 1, wb);
+            consume_step(k, wa);
+            if (k + 2 < nsteps) load_step(k + 2, wa);
+            consume_step(k + 1, wb);
+        }
+        if (k < nsteps) consume_step(k, wa);
+    } else {
+        for (int k = 0; k < nsteps; ++k) {
+            if (k > 0) load_step(k, wa);
+            consume_step(k, wa);
+        }
     }
     epi.finish(smem);
 }
@@ -452,10 +485,10 @@ inline int gemv_blocks(int units) {
     return b < kGemvMaxBlocks ? (b > 0 ? b : 1) : kGemvMaxBlocks;
 }
 
-template <typename WT, int R, int U, bool NT, bool CMB = false, class Epi>
+template <typename WT, int R, int U, bool NT, bool CMB = false, bool DB = (R * U <= 8), class Epi>
 hipError_t launch_gemv(const WT* W, const GemvIn& in, const Epi& epi, int units, hipStream_t s) {
     const size_t lds = gemv_lds_bytes(in.cols) + (CMB ? gemv_combine_lds(in) : 0);
-    hipLaunchKernelGGL((gemv_kernel<WT, R, U, NT, Epi, CMB>), dim3(gemv_blocks(units)), dim3(kGemvThreads), lds, s,
+    hipLaunchKernelGGL((gemv_kernel<WT, R, U, NT, Epi, CMB, DB>), dim3(gemv_blocks(units)), dim3(kGemvThreads), lds, s,
                        W, in, epi);
     return hipGetLastError();
 }

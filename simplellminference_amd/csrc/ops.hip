@@ -165,14 +165,15 @@ int attn_wg_positions(int kv_dtype, int head_dim) { return kAttnWaves * mha_ppw(
 template <typename KT, int HD>
 static int mha_launch_hd(const float* q, const KT* kc, const KT* vc, float* out, int layer, int pos, const int32_t* pos_dev,
                          int T, int H, int Hkv, long long pos_stride, long long head_stride, long long layer_stride,
-                         float* part, bool combine, hipStream_t s) {
+                         float* part, bool combine, hipStream_t s, const StreamPrefetch& pf) {
     using Geo = AttnGeom<KT, HD>;
     constexpr int ppw_wg = kAttnWaves * Geo::PPW;
     const int wg_splits = (T + ppw_wg - 1) / ppw_wg;
     if (wg_splits > kAttnMaxWgSplits) return fail(SLI_ERR_SHAPE, "mha: context too long for the combine kernel");
     AttnArgs<KT> a{q, kc + (long long)layer * layer_stride, vc + (long long)layer * layer_stride, pos_stride,
-                   head_stride, part, pos_dev, pos, Hkv, wg_splits, 1.0f / sqrtf((float)HD)};
-    const int blocks = Hkv * wg_splits;
+                   head_stride, part, pos_dev, pos, Hkv, wg_splits, 1.0f / sqrtf((float)HD), pf};
+    if (pf.bytes < 16 * (long long)pf.blocks) a.pf.blocks = 0;
+    const int blocks = Hkv * wg_splits + a.pf.blocks;
     const int g = H / Hkv;
     switch (g) {
         case 1: hipLaunchKernelGGL((attn_partial_kernel<KT, HD, 1>), dim3(blocks), dim3(256), 0, s, a); break;
@@ -182,7 +183,7 @@ static int mha_launch_hd(const float* q, const KT* kc, const KT* vc, float* out,
         default: return fail(SLI_ERR_SHAPE, "mha: heads per kv head must be 1, 2, 4 or 8");
     }
     SLI_HIP(hipGetLastError());
-    if (!combine) return SLI_OK;  // the consumer merges the partials itself (gemv_stage_combine)
+    if (!combine) return SLI_OK;  // the consumer merges the partials itself (CombineStage)
     hipLaunchKernelGGL((attn_combine_kernel<HD>), dim3(H), dim3(128), 0, s, part, out, pos_dev, pos, wg_splits,
                        ppw_wg);
     SLI_HIP(hipGetLastError());
@@ -192,20 +193,22 @@ static int mha_launch_hd(const float* q, const KT* kc, const KT* vc, float* out,
 template <typename KT>
 int mha_launch(const float* q, const KT* kc, const KT* vc, float* out, int layer, int pos, const int32_t* pos_dev,
                int T, int hd, int H, int Hkv, long long pos_stride, long long head_stride, long long layer_stride,
-               float* part, hipStream_t s, bool combine) {
+               float* part, hipStream_t s, bool combine, const StreamPrefetch& pf) {
     if (hd == 128)
         return mha_launch_hd<KT, 128>(q, kc, vc, out, layer, pos, pos_dev, T, H, Hkv, pos_stride, head_stride,
-                                      layer_stride, part, combine, s);
+                                      layer_stride, part, combine, s, pf);
     if (hd == 64)
         return mha_launch_hd<KT, 64>(q, kc, vc, out, layer, pos, pos_dev, T, H, Hkv, pos_stride, head_stride,
-                                     layer_stride, part, combine, s);
+                                     layer_stride, part, combine, s, pf);
     return fail(SLI_ERR_SHAPE, "mha: head_dim must be 64 or 128");
 }
 
 template int mha_launch<float>(const float*, const float*, const float*, float*, int, int, const int32_t*, int, int,
-                               int, int, long long, long long, long long, float*, hipStream_t, bool);
+                               int, int, long long, long long, long long, float*, hipStream_t, bool,
+                               const StreamPrefetch&);
 template int mha_launch<__half>(const float*, const __half*, const __half*, float*, int, int, const int32_t*, int,
-                                int, int, int, long long, long long, long long, float*, hipStream_t, bool);
+                                int, int, int, long long, long long, long long, float*, hipStream_t, bool,
+                                const StreamPrefetch&);
 
 size_t mha_workspace_bytes(int T, int H, int hd) {
     const int ppw_wg_min = kAttnWaves * mha_ppw(SLI_DT_F32, hd);

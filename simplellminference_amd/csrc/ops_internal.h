@@ -1,5 +1,6 @@
 // ops_internal.h — launchers shared between the kernel-level ABI (ops.hip) and the engine (engine.hip).
 #pragma once
+#include "attention.h"
 #include "common.h"
 
 namespace sli {
@@ -7,7 +8,7 @@ namespace sli {
 template <typename KT>
 int mha_launch(const float* q, const KT* kc, const KT* vc, float* out, int layer, int pos, const int32_t* pos_dev,
                int T, int hd, int H, int Hkv, long long pos_stride, long long head_stride, long long layer_stride,
-               float* part, hipStream_t s, bool combine = true);
+               float* part, hipStream_t s, bool combine = true, const StreamPrefetch& pf = StreamPrefetch{});
 
 size_t mha_workspace_bytes(int T, int H, int hd);
 int attn_wg_positions(int kv_dtype, int head_dim);  // context positions per attention workgroup

@@ -39,19 +39,6 @@ def test_tiny_predict_parity(gpu, oracle, name, w, kv, tol):
     gm.close()
 
 
-@pytest.mark.parametrize("name", ["tiny", "tiny-gqa"])
-@pytest.mark.parametrize("w,kv,tol", [("f16", "f16", 1e-3), ("i8", "f16", 1e-3), ("f32", "f32", 1e-4)])
-def test_persistent_step_parity(gpu, oracle, monkeypatch, name, w, kv, tol):
-    """SLI_STEP_MODE=persistent: the whole step as one persistent launch with grid barriers (opt-in)."""
-    monkeypatch.setenv("SLI_STEP_MODE", "persistent")
-    om, gm = _models(oracle, name, w, kv)
-    otok, olog = om.predict(PROMPT, 36)
-    gtok, glog = gm.predict(PROMPT, 36, want_logits=True)
-    gm.close()
-    assert np.array_equal(gtok, otok), (gtok, otok)
-    assert np.abs(glog - olog).max() <= tol
-
-
 def test_forward_is_idempotent_and_matches_predict(gpu, oracle):
     om, gm = _models(oracle, "tiny-gqa", "f16", "f16")
     toks, logits = gm.predict(PROMPT, 12, want_logits=True)

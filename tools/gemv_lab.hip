@@ -1,0 +1,196 @@
+// gemv_lab.hip — diagnostic: GEMV configurations (rows per unit R, vectors in flight U, double
+// buffering) on the Llama-2-7B decode shapes (fp16 weights, fp32 x), each timed over NL distinct layers
+// inside a replayed hipGraph so no launch re-reads weights from the Infinity Cache. Prints µs per launch
+// and GB/s of algorithmic weight bytes, a pure streaming-read kernel as the per-shape ceiling, and the
+// 4-GEMV layer chain for chosen per-shape configurations.
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include tools/gemv_lab.hip -o tools/gemv_lab
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../simplellminference_amd/csrc/gemv.h"
+
+using namespace sli;
+
+#define CK(x)                                                                               \
+    do {                                                                                    \
+        hipError_t e_ = (x);                                                                \
+        if (e_ != hipSuccess) {                                                             \
+            printf("%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_));        \
+            exit(1);                                                                        \
+        }                                                                                   \
+    } while (0)
+
+__global__ void fill_h(__half* p, size_t n, unsigned seed, float scale) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        unsigned h = (unsigned)i * 2654435761u ^ seed;
+        h ^= h >> 15;
+        h *= 2246822519u;
+        h ^= h >> 13;
+        p[i] = __float2half(((float)(h & 0xFFFF) / 65536.0f - 0.5f) * scale);
+    }
+}
+__global__ void fill_f(float* p, size_t n, unsigned seed) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        unsigned h = (unsigned)i * 2246822519u ^ seed;
+        h ^= h >> 13;
+        h *= 2654435761u;
+        h ^= h >> 16;
+        p[i] = (float)(h & 0xFFFF) / 65536.0f - 0.5f;
+    }
+}
+
+// pure streaming read: workgroup b reads its contiguous 1/grid of the bytes, U x 16 B per lane in flight
+template <int U>
+__global__ void __launch_bounds__(1024) stream_kernel(const char* p, long long bytes, float* out) {
+    const long long per = bytes / gridDim.x;
+    const char* b = p + per * blockIdx.x;
+    const int nvec = (int)(per / 16);
+    float acc = 0.0f;
+    for (int v = threadIdx.x; v < nvec; v += U * 1024) {
+        u32x4 w[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) w[j] = load16<true>(b + (size_t)min(v + j * 1024, nvec - 1) * 16);
+#pragma unroll
+        for (int j = 0; j < U; ++j) acc += __uint_as_float(w[j].x ^ w[j].y ^ w[j].z ^ w[j].w);
+    }
+    if (acc == 1.2345f) out[blockIdx.x] = acc;
+}
+
+struct Shape {
+    const char* name;
+    int rows, cols;
+};
+static const Shape kShapes[] = {{"qkv", 12288, 4096}, {"wo", 4096, 4096}, {"gu", 22016, 4096}, {"down", 4096, 11008},
+                                {"lm", 32000, 4096}};
+constexpr int NL = 20;
+
+struct Cfg {
+    const char* name;
+    std::function<void(const __half*, const GemvIn&, float*, int, hipStream_t)> run;
+};
+
+template <int R, int U, bool DB>
+static void run_cfg(const __half* W, const GemvIn& in, float* y, int rows, hipStream_t s) {
+    EpiStore<R> e{y, nullptr, nullptr, 1.0f, rows};
+    CK((launch_gemv<__half, R, U, true, false, DB>(W, in, e, (rows + R - 1) / R, s)));
+}
+
+static float time_graph(hipStream_t s, const std::function<void()>& body, int reps = 5) {
+    hipGraph_t g;
+    hipGraphExec_t ge;
+    CK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
+    body();
+    CK(hipStreamEndCapture(s, &g));
+    CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    CK(hipGraphLaunch(ge, s));
+    CK(hipStreamSynchronize(s));
+    hipEvent_t a, e;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&e));
+    CK(hipEventRecord(a, s));
+    for (int r = 0; r < reps; ++r) CK(hipGraphLaunch(ge, s));
+    CK(hipEventRecord(e, s));
+    CK(hipEventSynchronize(e));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, e));
+    CK(hipGraphExecDestroy(ge));
+    CK(hipGraphDestroy(g));
+    return ms / reps;
+}
+
+int main(int argc, char** argv) {
+    hipStream_t s;
+    CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    std::vector<__half*> w[5];
+    for (int si = 0; si < 5; ++si) {
+        const size_t n = (size_t)kShapes[si].rows * kShapes[si].cols;
+        const int layers = si == 4 ? 4 : NL;
+        for (int l = 0; l < layers; ++l) {
+            __half* p;
+            CK(hipMalloc(&p, n * 2));
+            hipLaunchKernelGGL(fill_h, dim3(4096), dim3(256), 0, s, p, n, 77u + si * 1000 + l, 0.05f);
+            w[si].push_back(p);
+        }
+    }
+    float *x, *nw, *y, *y2;
+    CK(hipMalloc(&x, 16384 * 4));
+    CK(hipMalloc(&nw, 16384 * 4));
+    CK(hipMalloc(&y, 32768 * 4));
+    CK(hipMalloc(&y2, 32768 * 4));
+    hipLaunchKernelGGL(fill_f, dim3(64), dim3(256), 0, s, x, 16384, 5u);
+    hipLaunchKernelGGL(fill_f, dim3(64), dim3(256), 0, s, nw, 16384, 9u);
+    CK(hipStreamSynchronize(s));
+
+    std::vector<Cfg> cfgs = {
+        {"R2U8", run_cfg<2, 8, false>},    {"R2U4 DB", run_cfg<2, 4, true>}, {"R1U8 DB", run_cfg<1, 8, true>},
+        {"R1U8", run_cfg<1, 8, false>},    {"R1U16", run_cfg<1, 16, false>}, {"R2U4", run_cfg<2, 4, false>},
+        {"R1U4 DB", run_cfg<1, 4, true>},  {"R4U2 DB", run_cfg<4, 2, true>},
+    };
+    auto in_for = [&](int si) { return GemvIn{x, si == 3 ? nullptr : nw, 1e-5f, kShapes[si].cols}; };
+
+    // correctness against the first configuration
+    std::vector<float> h1(32768), h2(32768);
+    for (int si = 0; si < 5; ++si) {
+        cfgs[0].run(w[si][0], in_for(si), y, kShapes[si].rows, s);
+        CK(hipStreamSynchronize(s));
+        CK(hipMemcpy(h1.data(), y, 4 * kShapes[si].rows, hipMemcpyDeviceToHost));
+        for (size_t c = 1; c < cfgs.size(); ++c) {
+            cfgs[c].run(w[si][0], in_for(si), y2, kShapes[si].rows, s);
+            CK(hipStreamSynchronize(s));
+            CK(hipMemcpy(h2.data(), y2, 4 * kShapes[si].rows, hipMemcpyDeviceToHost));
+            double md = 0, mx = 0;
+            for (int r = 0; r < kShapes[si].rows; ++r) {
+                md = fmax(md, fabs((double)h1[r] - h2[r]));
+                mx = fmax(mx, fabs((double)h1[r]));
+            }
+            if (md > 1e-4 * (mx + 1)) printf("MISMATCH %s %s max|diff| %.3e\n", kShapes[si].name, cfgs[c].name, md);
+        }
+    }
+    std::vector<std::vector<double>> us_tab(5, std::vector<double>(cfgs.size()));
+    for (int si = 0; si < 5; ++si) {
+        const int layers = (int)w[si].size();
+        const double bytes = (double)kShapes[si].rows * kShapes[si].cols * 2;
+        for (size_t c = 0; c < cfgs.size(); ++c) {
+            const float ms = time_graph(s, [&] {
+                for (int l = 0; l < layers; ++l) cfgs[c].run(w[si][l], in_for(si), y, kShapes[si].rows, s);
+            });
+            const double us = 1000.0 * ms / layers;
+            us_tab[si][c] = us;
+            printf("%-5s %-9s %8.2f us  %7.1f GB/s\n", kShapes[si].name, cfgs[c].name, us, bytes / (us * 1e-6) / 1e9);
+        }
+        const float ms = time_graph(s, [&] {
+            for (int l = 0; l < layers; ++l)
+                hipLaunchKernelGGL(stream_kernel<8>, dim3(256), dim3(1024), 0, s, (const char*)w[si][l],
+                                   (long long)kShapes[si].rows * kShapes[si].cols * 2, y2);
+        });
+        const double us = 1000.0 * ms / layers;
+        printf("%-5s %-9s %8.2f us  %7.1f GB/s\n", kShapes[si].name, "stream", us, bytes / (us * 1e-6) / 1e9);
+    }
+    // layer chain with the best configuration per shape vs the baseline
+    std::vector<int> best(4, 0);
+    for (int si = 0; si < 4; ++si)
+        for (size_t c = 0; c < cfgs.size(); ++c)
+            if (us_tab[si][c] < us_tab[si][best[si]]) best[si] = (int)c;
+    const double lbytes = 2.0 * (12288.0 * 4096 + 4096.0 * 4096 + 22016.0 * 4096 + 4096.0 * 11008);
+    for (int pick = 0; pick < 2; ++pick) {
+        const float ms = time_graph(s, [&] {
+            for (int l = 0; l < NL; ++l)
+                for (int si = 0; si < 4; ++si) {
+                    const int c = pick ? best[si] : 0;
+                    cfgs[c].run(w[si][l], in_for(si), y, kShapes[si].rows, s);
+                }
+        });
+        const double us = 1000.0 * ms / NL;
+        printf("layer chain %s: %8.2f us/layer  %7.1f GB/s  [", pick ? "best" : "R2U8", us, lbytes / (us * 1e-6) / 1e9);
+        for (int si = 0; si < 4; ++si) printf(" %s=%s", kShapes[si].name, cfgs[pick ? best[si] : 0].name);
+        printf(" ]\n");
+    }
+    return 0;
+}
