@@ -60,27 +60,33 @@ struct AttnArgs {
     StreamPrefetch pf;      // optional: workgroups past n_kv_heads * max_splits prefetch this range
 };
 
-constexpr int kAttnNit = 16;  // 16-byte vectors per lane per operand per wave (K and V each)
+// A workgroup covers kAttnSlots wave-instructions of K (and of V) per lane-row group: WAVES waves of
+// NIT = kAttnSlots / WAVES vectors each. The split geometry (positions per workgroup) is therefore the
+// same for every WAVES; WAVES trades registers for latency hiding: 16 waves of 4 (MHA, GQA-2: each
+// wave starts computing as soon as its own few rows land, 4 waves per SIMD overlap) or 4 waves of 16
+// (GQA-4/8, whose G query heads need the register room of one wave per SIMD).
+constexpr int kAttnSlots = 64;
+constexpr int kAttnMaxWgSplits = 128;  // combine-kernel capacity
 
 template <typename KT, int HD>
 struct AttnGeom {
     static constexpr int EPV = Vec16<KT>::N;
     static constexpr int LPR = HD / EPV;     // lanes per cached row
     static constexpr int RPI = 64 / LPR;     // rows per wave-instruction
-    static constexpr int PPW = kAttnNit * RPI;  // positions per wave (context slice)
+    static constexpr int PPWG = kAttnSlots * RPI;  // positions per workgroup (context split)
     static_assert(LPR >= 1 && LPR <= 64 && (64 % LPR) == 0, "head_dim / vector shape");
 };
 
-constexpr int kAttnWaves = 4;        // waves per workgroup = consecutive context slices of one kv head
-constexpr int kAttnMaxWgSplits = 128; // combine-kernel capacity (ctx <= 128 * 4 * PPW)
+__host__ __device__ constexpr int attn_waves(int g) { return g <= 2 ? 16 : 4; }
 
-// grid: n_kv_heads * wg_splits workgroups; wave w of workgroup (kvh, s) owns context slice 4s + w.
-// The 4 slice states are merged in LDS, so one partial per (q head, workgroup) reaches the workspace.
+// grid: n_kv_heads * wg_splits workgroups; wave w of workgroup (kvh, s) owns the w-th slice of split s.
+// The WAVES slice states are merged in LDS, so one partial per (q head, workgroup) reaches the workspace.
 template <typename KT, int HD, int G>
-__global__ void __launch_bounds__(256) attn_partial_kernel(AttnArgs<KT> a) {
+__global__ void __launch_bounds__(64 * attn_waves(G)) attn_partial_kernel(AttnArgs<KT> a) {
     using Geo = AttnGeom<KT, HD>;
-    constexpr int EPV = Geo::EPV, LPR = Geo::LPR, RPI = Geo::RPI, PPW = Geo::PPW;
-    __shared__ float sh[kAttnWaves][G][HD + 2];
+    constexpr int WAVES = attn_waves(G), kAttnNit = kAttnSlots / WAVES;
+    constexpr int EPV = Geo::EPV, LPR = Geo::LPR, RPI = Geo::RPI, PPW = kAttnNit * RPI;
+    __shared__ float sh[WAVES][G][HD + 2];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     if ((int)blockIdx.x >= a.n_kv_heads * a.max_splits) {
@@ -90,8 +96,8 @@ __global__ void __launch_bounds__(256) attn_partial_kernel(AttnArgs<KT> a) {
     const int kvh = blockIdx.x / a.max_splits;  // max_splits counts workgroup splits here
     const int wgs = blockIdx.x - kvh * a.max_splits;
     const int pos = a.pos_dev ? *a.pos_dev : a.pos_host;
-    if (wgs * kAttnWaves * PPW > pos) return;  // whole workgroup past the live context (uniform exit)
-    const int t0 = (wgs * kAttnWaves + wave) * PPW;
+    if (wgs * WAVES * PPW > pos) return;  // whole workgroup past the live context (uniform exit)
+    const int t0 = (wgs * WAVES + wave) * PPW;
     const bool live_wave = t0 <= pos;
     const int t_end = min(t0 + PPW, pos + 1);
     const int sub = lane / LPR;
@@ -183,10 +189,10 @@ __global__ void __launch_bounds__(256) attn_partial_kernel(AttnArgs<KT> a) {
         const int g = i / HD, d = i - g * HD;
         float M = -INFINITY;
 #pragma unroll
-        for (int w = 0; w < kAttnWaves; ++w) M = fmaxf(M, sh[w][g][HD]);
+        for (int w = 0; w < WAVES; ++w) M = fmaxf(M, sh[w][g][HD]);
         float o = 0.0f, L = 0.0f;
 #pragma unroll
-        for (int w = 0; w < kAttnWaves; ++w) {
+        for (int w = 0; w < WAVES; ++w) {
             const float c = expf(sh[w][g][HD] - M);  // dead waves: m = -inf -> 0
             o = fmaf(c, sh[w][g][d], o);
             L = fmaf(c, sh[w][g][HD + 1], L);

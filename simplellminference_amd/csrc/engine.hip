@@ -309,7 +309,7 @@ struct StepRecorder {
         const LayerW& w = m->layers[l];
         GemvIn in{m->x, m->norms + (size_t)(2 * l + 1) * m->D, m->c.eps, m->D};
         EpiSwiGLU e{m->act, w.gu_s, m->Il, m->c.act_mode};
-        SLI_HIP((launch_gemv<WT, 2, 4, NT, false, false>((const WT*)w.gu, in, e, m->Il, m->stream)));
+        SLI_HIP((launch_gemv<WT, 2, 8, NT, false, false>((const WT*)w.gu, in, e, m->Il, m->stream)));
         return SLI_OK;
     }
     static int gemv_down(sli_model* m, int l) {

@@ -27,6 +27,7 @@ struct GemvIn {
     const float* part = nullptr;   // [cols / hd][max_splits][hd + kAttnPartPad]
     const int32_t* pos = nullptr;  // live splits = *pos / ppw_wg + 1
     int hd = 0, max_splits = 0, ppw_wg = 0;
+    unsigned long long* stamps = nullptr;  // diagnostic (tools/gemv_lab): per-wave s_memrealtime x4
 };
 
 constexpr int kGemvThreads = 1024;  // one persistent 16-wave workgroup per CU: x staged once per CU
@@ -47,36 +48,33 @@ struct XStage {
     __device__ __forceinline__ void issue(const GemvIn& in) {
         const int tid = threadIdx.x, nt = blockDim.x, n4 = in.cols >> 2;
         const float4* x4 = reinterpret_cast<const float4*>(in.x);
+        // unconditional (clamped) loads: a load under a branch would make the weight waits conservative
+        const float4* w4 = reinterpret_cast<const float4*>(in.norm_w ? in.norm_w : in.x);
 #pragma unroll
-        for (int k = 0; k < kGemvStageV4; ++k)  // k * nt < n4 is uniform; the clamp covers the ragged tail
-            if (k * nt < n4) xr[k] = x4[min(tid + k * nt, n4 - 1)];
-        if (in.norm_w != nullptr) {
-            const float4* w4 = reinterpret_cast<const float4*>(in.norm_w);
-#pragma unroll
-            for (int k = 0; k < kGemvStageV4; ++k)
-                if (k * nt < n4) wr[k] = w4[min(tid + k * nt, n4 - 1)];
+        for (int k = 0; k < kGemvStageV4; ++k) {
+            xr[k] = x4[min(tid + k * nt, n4 - 1)];
+            wr[k] = w4[min(tid + k * nt, n4 - 1)];
         }
     }
-    // x (optionally RMS-normalised, rms_kernel.cpp:5-23) into LDS; the caller then barriers.
+    // x (optionally RMS-normalised, rms_kernel.cpp:5-23) into LDS; the caller then barriers. Stores are
+    // unconditional too (clamped rounds rewrite the last vector with its own value).
     __device__ __forceinline__ void commit(float* smem, const GemvIn& in) {
         float* red = smem;
-        float* xs = smem + kGemvLdsHead;
+        float4* xs4 = reinterpret_cast<float4*>(smem + kGemvLdsHead);
         const int tid = threadIdx.x, nt = blockDim.x, n4 = in.cols >> 2;
         if (in.norm_w == nullptr) {
 #pragma unroll
-            for (int k = 0; k < kGemvStageV4; ++k)
-                if (tid + k * nt < n4) reinterpret_cast<float4*>(xs)[tid + k * nt] = xr[k];
+            for (int k = 0; k < kGemvStageV4; ++k) xs4[min(tid + k * nt, n4 - 1)] = xr[k];
             return;
         }
         float ss = 0.0f;
 #pragma unroll
         for (int k = 0; k < kGemvStageV4; ++k) {
-            if (tid + k * nt < n4) {
-                ss += xr[k].x * xr[k].x;
-                ss += xr[k].y * xr[k].y;
-                ss += xr[k].z * xr[k].z;
-                ss += xr[k].w * xr[k].w;
-            }
+            const float m = tid + k * nt < n4 ? 1.0f : 0.0f;
+            ss += m * (xr[k].x * xr[k].x);
+            ss += m * (xr[k].y * xr[k].y);
+            ss += m * (xr[k].z * xr[k].z);
+            ss += m * (xr[k].w * xr[k].w);
         }
         ss = wave_sum(ss);
         if ((tid & 63) == 0) red[tid >> 6] = ss;
@@ -91,24 +89,23 @@ struct XStage {
         __syncthreads();
         const float inv = red[32];
 #pragma unroll
-        for (int k = 0; k < kGemvStageV4; ++k) {
-            if (tid + k * nt < n4) {  // :20-22  y = (x * inv) * w
-                float4 o;
-                o.x = (xr[k].x * inv) * wr[k].x;
-                o.y = (xr[k].y * inv) * wr[k].y;
-                o.z = (xr[k].z * inv) * wr[k].z;
-                o.w = (xr[k].w * inv) * wr[k].w;
-                reinterpret_cast<float4*>(xs)[tid + k * nt] = o;
-            }
+        for (int k = 0; k < kGemvStageV4; ++k) {  // :20-22  y = (x * inv) * w
+            float4 o;
+            o.x = (xr[k].x * inv) * wr[k].x;
+            o.y = (xr[k].y * inv) * wr[k].y;
+            o.z = (xr[k].z * inv) * wr[k].z;
+            o.w = (xr[k].w * inv) * wr[k].w;
+            xs4[min(tid + k * nt, n4 - 1)] = o;
         }
     }
 };
 
 // Merge the attention partials straight into the staged x (replaces attn_combine_kernel and its launch):
 // x[h*hd + d] = sum_i e^{m_i - M} o_i[d] / sum_i e^{m_i - M} l_i over the live splits of head h, summed in
-// split order. issue(): this thread's first CH o rows and its first (m, l) pair; commit(): the (m, l)
-// table through LDS, then the merge (further o batches, when a head has more than CH splits, are loaded
-// there and queue behind the weights). LDS: staged x [cols], then the (m, l) table (gemv_combine_lds).
+// split order. issue(): this thread's 4 columns of every split's o row and one (m, l) pair of the
+// table; commit(): the (m, l) table through LDS, then the merge — no global access after issue(), so
+// the weight loads behind it keep an exact vmcnt. Host contract (gemv_combine_ok): cols <= 4 * threads,
+// live splits <= CH, heads * splits <= threads. LDS: staged x [cols], then the (m, l) table.
 struct CombineStage {
     static constexpr int CH = 8;
     float4 po[CH];
@@ -129,44 +126,38 @@ struct CombineStage {
     }
     __device__ __forceinline__ void commit(float* smem, const GemvIn& in) {
         float* xs = smem + kGemvLdsHead;
-        const int tid = threadIdx.x, nt = blockDim.x, ns = live(in);
+        const int tid = threadIdx.x, ns = live(in);
         const int n4 = in.cols >> 2, nml = (in.cols / in.hd) * ns;
         float2* mls = reinterpret_cast<float2*>(xs + in.cols);
         if (tid < nml) mls[tid] = ml0;
-        for (int k = tid + nt; k < nml; k += nt) {
-            const int h = k / ns, i = k - h * ns;
-            mls[k] = *reinterpret_cast<const float2*>(row(in, h, i) + in.hd);
-        }
         __syncthreads();
-        for (int c4 = tid; c4 < n4; c4 += nt) {
-            const int h = (c4 << 2) / in.hd, d = (c4 << 2) - h * in.hd;
+        if (tid < n4) {
+            const int h = (tid << 2) / in.hd;
             const float2* ml = mls + h * ns;
             float M = -INFINITY;
             for (int i = 0; i < ns; ++i) M = fmaxf(M, ml[i].x);
             float L = 0.0f;
             float4 o = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            for (int i0 = 0; i0 < ns; i0 += CH) {
-                if (c4 != tid || i0 != 0) {
 #pragma unroll
-                    for (int j = 0; j < CH; ++j)
-                        po[j] = *reinterpret_cast<const float4*>(row(in, h, min(i0 + j, ns - 1)) + d);
-                }
-#pragma unroll
-                for (int j = 0; j < CH; ++j) {
-                    if (i0 + j < ns) {
-                        const float w = expf(ml[i0 + j].x - M);
-                        o.x = fmaf(w, po[j].x, o.x);
-                        o.y = fmaf(w, po[j].y, o.y);
-                        o.z = fmaf(w, po[j].z, o.z);
-                        o.w = fmaf(w, po[j].w, o.w);
-                        L = fmaf(w, ml[i0 + j].y, L);
-                    }
+            for (int j = 0; j < CH; ++j) {
+                if (j < ns) {
+                    const float w = expf(ml[j].x - M);
+                    o.x = fmaf(w, po[j].x, o.x);
+                    o.y = fmaf(w, po[j].y, o.y);
+                    o.z = fmaf(w, po[j].z, o.z);
+                    o.w = fmaf(w, po[j].w, o.w);
+                    L = fmaf(w, ml[j].y, L);
                 }
             }
-            reinterpret_cast<float4*>(xs)[c4] = make_float4(o.x / L, o.y / L, o.z / L, o.w / L);
+            reinterpret_cast<float4*>(xs)[tid] = make_float4(o.x / L, o.y / L, o.z / L, o.w / L);
         }
     }
 };
+
+// Host check for the fused merge (CombineStage contract).
+inline bool gemv_combine_ok(int cols, int hd, int max_splits) {
+    return cols <= 4 * kGemvThreads && max_splits <= CombineStage::CH && (cols / hd) * max_splits <= kGemvThreads;
+}
 
 inline size_t gemv_combine_lds(const GemvIn& in) {
     return sizeof(float2) * (size_t)(in.cols / in.hd) * in.max_splits;
@@ -209,11 +200,30 @@ __device__ __forceinline__ void gemv_chunk(const u32x4 (&w)[U][R], const float* 
     }
 }
 
+// Units of workgroup b: [b*W*N/G, (b+1)*W*N/G) for W waves per workgroup, G workgroups (32-bit math:
+// grid waves x units stays below 2^32 for every supported shape).
+__device__ __forceinline__ int gemv_unit_begin(int gwave, int nunits, int total_waves) {
+    return (int)(((unsigned)gwave * (unsigned)nunits) / (unsigned)total_waves);
+}
+
+// Result slots in LDS behind the staged x (and the combine table): R floats per unit of the workgroup.
+inline size_t gemv_res_floats(int units, int grid, int R) {
+    return (size_t)R * ((size_t)units / grid + 2);
+}
+
 // Wave-level schedule. Wave gw of the grid owns units [gw*N/W, (gw+1)*N/W) (balanced: sizes differ by at
 // most one); a unit is R rows chosen by the epilogue, streamed in chunks of U 16-byte vectors per row
 // per lane. The wave's work is the flat sequence of (unit, chunk) steps; with DB the next step's loads
 // are issued before the current step is consumed (two register buffers), so each wave keeps a chunk in
-// flight while it computes and waves drift apart instead of stalling together at chunk boundaries.
+// flight while it computes.
+//
+// Straight-line memory order, no global access inside the loop but weight loads: every weight load is
+// unconditional (positions clamped to the wave's last step; a wave without units loads a valid row it
+// never uses), and finished row sums go to LDS, not to global memory. s_waitcnt vmcnt counts loads and
+// stores together in issue order, so a conditional load or store anywhere in the sequence forces the
+// compiler to a conservative vmcnt(0) at the next use of the weights — measured: the x prologue waited
+// for the first weight chunk (staged 4-6 us into a 10-30 us launch). The epilogue (residual reads,
+// RoPE, K/V writes, logits) runs once per workgroup after the loop, one thread per unit.
 // Prologue order: input loads, first weight chunk, input commit + barrier (see XStage).
 // CMB: stage x by merging attention partials (CombineStage) instead of reading in.x.
 template <typename WT, int R, int U, bool NT, class Epi, bool CMB = false, bool DB = (R * U <= 8)>
@@ -225,27 +235,33 @@ __global__ void __launch_bounds__(kGemvThreads) gemv_kernel(const WT* __restrict
     constexpr int EPV = Vec16<WT>::N;
     constexpr int CV = U * 64;  // vectors per row per chunk
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nwaves = blockDim.x >> 6;
     const int nvec = in.cols / EPV;
     const size_t row_bytes = (size_t)in.cols * sizeof(WT);
     const int nunits = epi.units();
-    const long long gw = (long long)blockIdx.x * nwaves + wave;
-    const long long nw = (long long)gridDim.x * nwaves;
-    const int u_begin = (int)(gw * nunits / nw);
-    const int u_end = (int)((gw + 1) * nunits / nw);
+    const int total_waves = gridDim.x * nwaves;
+    const int gw = blockIdx.x * nwaves + wave;
+    const int u_begin = gemv_unit_begin(gw, nunits, total_waves);
+    const int u_end = gemv_unit_begin(gw + 1, nunits, total_waves);
+    const int ub = gemv_unit_begin(blockIdx.x * nwaves, nunits, total_waves);  // workgroup's first unit
+    const int ue = gemv_unit_begin((blockIdx.x + 1) * nwaves, nunits, total_waves);
     const int cpr = (nvec + CV - 1) / CV;  // chunks per row
     const int nsteps = (u_end - u_begin) * cpr;
+    float* res = smem + kGemvLdsHead + in.cols + (CMB ? 2 * (in.cols / max(in.hd, 1)) * in.max_splits : 0);
 
+    const unsigned long long t_entry = in.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
     using Stage = typename std::conditional<CMB, CombineStage, XStage>::type;
     Stage stage;
     stage.issue(in);
+    __builtin_amdgcn_sched_barrier(0);  // keep every input load ahead of the weight loads
 
-    auto load_step = [&](int k, u32x4 (&w)[U][R]) {
-        const int u = u_begin + k / cpr;
-        const int v = (k % cpr) * CV + lane;
+    // (u, c) = unit and chunk of a step; the load position saturates at the wave's last step
+    const int u_last = max(min(u_end, nunits) - 1, 0);
+    auto load_step = [&](int u, int c, u32x4 (&w)[U][R]) {
         int rows[R];
-        epi.rows(u, rows);
+        epi.rows(min(u, u_last), rows);
+        const int v = (u > u_last ? cpr - 1 : c) * CV + lane;
 #pragma unroll
         for (int j = 0; j < U; ++j) {
             const int vj = min(v + j * 64, nvec - 1);  // clamp, never branch around a load
@@ -254,49 +270,78 @@ __global__ void __launch_bounds__(kGemvThreads) gemv_kernel(const WT* __restrict
                 w[j][r] = load16<NT>(reinterpret_cast<const char*>(W) + (size_t)rows[r] * row_bytes + (size_t)vj * 16);
         }
     };
+    auto next = [&](int& u, int& c) {
+        if (++c == cpr) {
+            c = 0;
+            ++u;
+        }
+    };
     float acc[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = 0.0f;
-    auto consume_step = [&](int k, const u32x4(&w)[U][R]) {
-        const int c = k % cpr;
+    auto consume_step = [&](int u, int c, const u32x4(&w)[U][R]) {
         const int v = c * CV + lane;
         if ((c + 1) * CV <= nvec)
             gemv_chunk<WT, R, U>(w, xs, v, acc);
         else
             gemv_chunk<WT, R, U, true>(w, xs, v, acc, nvec);
-        if (c == cpr - 1) {  // unit complete
-            const int u = u_begin + k / cpr;
-            int rows[R];
-            epi.rows(u, rows);
+        if (c == cpr - 1) {  // unit complete: its R row sums go to LDS
 #pragma unroll
-            for (int r = 0; r < R; ++r) acc[r] = wave_sum(acc[r]);
-            epi.store(u, rows, acc, lane);
-#pragma unroll
-            for (int r = 0; r < R; ++r) acc[r] = 0.0f;
+            for (int r = 0; r < R; ++r) {
+                const float t = wave_sum(acc[r]);
+                if (lane == 0) res[(u - ub) * R + r] = t;
+                acc[r] = 0.0f;
+            }
         }
     };
 
     u32x4 wa[U][R];
-    if (nsteps > 0) load_step(0, wa);
+    int lu = u_begin, lc = 0;  // next step to load
+    int cu = u_begin, cc = 0;  // next step to consume
+    load_step(lu, lc, wa);
+    next(lu, lc);
+    __builtin_amdgcn_sched_barrier(0);
     stage.commit(smem, in);
     __syncthreads();
+    const unsigned long long t_staged = in.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
     if constexpr (DB) {
         u32x4 wb[U][R];
         int k = 0;
         for (; k + 1 < nsteps; k += 2) {
-            load_step(k + 1, wb);
-            consume_step(k, wa);
-            if (k + 2 < nsteps) load_step(k + 2, wa);
-            consume_step(k + 1, wb);
+            load_step(lu, lc, wb);
+            next(lu, lc);
+            consume_step(cu, cc, wa);
+            next(cu, cc);
+            load_step(lu, lc, wa);  // past the end: a clamped re-read, never consumed
+            next(lu, lc);
+            consume_step(cu, cc, wb);
+            next(cu, cc);
         }
-        if (k < nsteps) consume_step(k, wa);
+        if (k < nsteps) consume_step(cu, cc, wa);
     } else {
         for (int k = 0; k < nsteps; ++k) {
-            if (k > 0) load_step(k, wa);
-            consume_step(k, wa);
+            if (k > 0) {
+                load_step(lu, lc, wa);
+                next(lu, lc);
+            }
+            consume_step(cu, cc, wa);
+            next(cu, cc);
         }
     }
+    __syncthreads();
+    for (int u = ub + (int)threadIdx.x; u < ue; u += blockDim.x) {
+        int rows[R];
+        epi.rows(u, rows);
+        epi.store(u, rows, res + (u - ub) * R);
+    }
     epi.finish(smem);
+    if (in.stamps && lane == 0) {
+        unsigned long long* p = in.stamps + ((size_t)blockIdx.x * nwaves + wave) * 4;
+        p[0] = t_entry;
+        p[1] = t_staged;
+        p[2] = __builtin_amdgcn_s_memrealtime();
+        p[3] = (unsigned long long)max(nsteps, 1);
+    }
 }
 
 // Row-by-row fallback for shapes the vector kernel cannot take (cols*sizeof(WT) not a multiple of 16
@@ -317,7 +362,8 @@ __global__ void __launch_bounds__(kGemvThreads)
 }
 
 // ---------------------------------------------------------------- epilogues
-// Common shape: units(), rows(u, rows[R]), store(u, rows, acc[R], lane), finish(smem).
+// Common shape: units(), rows(u, rows[R]), store(u, rows, v[R]) (one thread per unit, final row sums),
+// finish(smem) (every thread of the workgoup).
 
 // y[row] = resid[row] + (sum * rscale[row]) * scale     (resid / rscale optional)
 // matmul_kernel.cpp:26 (sum*scale) fused with add_kernel.cpp:5-14 (residual add, model.cpp:86-90/124-128).
@@ -333,12 +379,12 @@ struct EpiStore {
 #pragma unroll
         for (int i = 0; i < R; ++i) r[i] = min(u * R + i, nrows - 1);
     }
-    __device__ void store(int u, const int*, const float* acc, int lane) const {
+    __device__ void store(int u, const int*, const float* v) const {
 #pragma unroll
         for (int i = 0; i < R; ++i) {
             const int row = u * R + i;
-            if (lane == i && row < nrows) {
-                float a = rscale ? acc[i] * rscale[row] : acc[i];
+            if (row < nrows) {
+                float a = rscale ? v[i] * rscale[row] : v[i];
                 a = a * scale;
                 y[row] = resid ? resid[row] + a : a;
             }
@@ -369,8 +415,7 @@ struct EpiQKV {
         r[0] = uh * hd + d;
         r[1] = uh * hd + d + half;
     }
-    __device__ void store(int u, const int* r, const float* acc, int lane) const {
-        if (lane != 0) return;
+    __device__ void store(int u, const int* r, const float* acc) const {
         const int half = hd / 2;
         const int uh = u / half;
         const int d = u - uh * half;
@@ -414,8 +459,7 @@ struct EpiSwiGLU {
         r[0] = u;
         r[1] = inter + u;
     }
-    __device__ void store(int u, const int* r, const float* acc, int lane) const {
-        if (lane != 0) return;
+    __device__ void store(int u, const int* r, const float* acc) const {
         float g = acc[0], up = acc[1];
         if (rscale) {
             g *= rscale[r[0]];
@@ -444,13 +488,13 @@ struct EpiLogits {
 #pragma unroll
         for (int i = 0; i < R; ++i) r[i] = min(u * R + i, nrows - 1);
     }
-    __device__ void store(int u, const int*, const float* acc, int lane) {
+    __device__ void store(int u, const int*, const float* acc) {
 #pragma unroll
         for (int i = 0; i < R; ++i) {
             const int row = u * R + i;
             if (row < nrows) {
                 const float a = rscale ? acc[i] * rscale[row] : acc[i];
-                if (lane == i) logits[row] = a;
+                logits[row] = a;
                 const unsigned long long k = argmax_key(a, (unsigned)(row + vocab_off));
                 best = k > best ? k : best;
             }
@@ -458,6 +502,7 @@ struct EpiLogits {
     }
     __device__ void finish(float* smem) {
         unsigned long long* red = reinterpret_cast<unsigned long long*>(smem);
+        best = wave_max_u64(best);
         __syncthreads();
         const int wave = threadIdx.x >> 6;
         if ((threadIdx.x & 63) == 0) red[wave] = best;
@@ -487,9 +532,10 @@ inline int gemv_blocks(int units) {
 
 template <typename WT, int R, int U, bool NT, bool CMB = false, bool DB = (R * U <= 8), class Epi>
 hipError_t launch_gemv(const WT* W, const GemvIn& in, const Epi& epi, int units, hipStream_t s) {
-    const size_t lds = gemv_lds_bytes(in.cols) + (CMB ? gemv_combine_lds(in) : 0);
-    hipLaunchKernelGGL((gemv_kernel<WT, R, U, NT, Epi, CMB, DB>), dim3(gemv_blocks(units)), dim3(kGemvThreads), lds, s,
-                       W, in, epi);
+    const int grid = gemv_blocks(units);
+    const size_t lds = gemv_lds_bytes(in.cols) + (CMB ? gemv_combine_lds(in) : 0) +
+                       sizeof(float) * gemv_res_floats(units, grid, R);
+    hipLaunchKernelGGL((gemv_kernel<WT, R, U, NT, Epi, CMB, DB>), dim3(grid), dim3(kGemvThreads), lds, s, W, in, epi);
     return hipGetLastError();
 }
 

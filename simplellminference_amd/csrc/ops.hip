@@ -155,19 +155,17 @@ static int matmul_dispatch(const float* x, const WT* w, const float* rscale, flo
     return SLI_OK;
 }
 
-static int mha_ppw(int kv_dtype, int head_dim) {
+int attn_wg_positions(int kv_dtype, int head_dim) {
     const int epv = kv_dtype == SLI_DT_F16 ? 8 : 4;
-    return kAttnNit * (64 / (head_dim / epv));
+    return kAttnSlots * (64 / (head_dim / epv));
 }
-
-int attn_wg_positions(int kv_dtype, int head_dim) { return kAttnWaves * mha_ppw(kv_dtype, head_dim); }
 
 template <typename KT, int HD>
 static int mha_launch_hd(const float* q, const KT* kc, const KT* vc, float* out, int layer, int pos, const int32_t* pos_dev,
                          int T, int H, int Hkv, long long pos_stride, long long head_stride, long long layer_stride,
                          float* part, bool combine, hipStream_t s, const StreamPrefetch& pf) {
     using Geo = AttnGeom<KT, HD>;
-    constexpr int ppw_wg = kAttnWaves * Geo::PPW;
+    constexpr int ppw_wg = Geo::PPWG;
     const int wg_splits = (T + ppw_wg - 1) / ppw_wg;
     if (wg_splits > kAttnMaxWgSplits) return fail(SLI_ERR_SHAPE, "mha: context too long for the combine kernel");
     AttnArgs<KT> a{q, kc + (long long)layer * layer_stride, vc + (long long)layer * layer_stride, pos_stride,
@@ -176,10 +174,10 @@ static int mha_launch_hd(const float* q, const KT* kc, const KT* vc, float* out,
     const int blocks = Hkv * wg_splits + a.pf.blocks;
     const int g = H / Hkv;
     switch (g) {
-        case 1: hipLaunchKernelGGL((attn_partial_kernel<KT, HD, 1>), dim3(blocks), dim3(256), 0, s, a); break;
-        case 2: hipLaunchKernelGGL((attn_partial_kernel<KT, HD, 2>), dim3(blocks), dim3(256), 0, s, a); break;
-        case 4: hipLaunchKernelGGL((attn_partial_kernel<KT, HD, 4>), dim3(blocks), dim3(256), 0, s, a); break;
-        case 8: hipLaunchKernelGGL((attn_partial_kernel<KT, HD, 8>), dim3(blocks), dim3(256), 0, s, a); break;
+        case 1: hipLaunchKernelGGL((attn_partial_kernel<KT, HD, 1>), dim3(blocks), dim3(64 * attn_waves(1)), 0, s, a); break;
+        case 2: hipLaunchKernelGGL((attn_partial_kernel<KT, HD, 2>), dim3(blocks), dim3(64 * attn_waves(2)), 0, s, a); break;
+        case 4: hipLaunchKernelGGL((attn_partial_kernel<KT, HD, 4>), dim3(blocks), dim3(64 * attn_waves(4)), 0, s, a); break;
+        case 8: hipLaunchKernelGGL((attn_partial_kernel<KT, HD, 8>), dim3(blocks), dim3(64 * attn_waves(8)), 0, s, a); break;
         default: return fail(SLI_ERR_SHAPE, "mha: heads per kv head must be 1, 2, 4 or 8");
     }
     SLI_HIP(hipGetLastError());
@@ -211,7 +209,7 @@ template int mha_launch<__half>(const float*, const __half*, const __half*, floa
                                 const StreamPrefetch&);
 
 size_t mha_workspace_bytes(int T, int H, int hd) {
-    const int ppw_wg_min = kAttnWaves * mha_ppw(SLI_DT_F32, hd);
+    const int ppw_wg_min = attn_wg_positions(SLI_DT_F32, hd);
     const size_t splits = (size_t)((T + ppw_wg_min - 1) / ppw_wg_min);
     return sizeof(float) * (size_t)H * splits * (size_t)(hd + kAttnPartPad);
 }

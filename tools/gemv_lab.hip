@@ -48,7 +48,9 @@ __global__ void fill_f(float* p, size_t n, unsigned seed) {
 
 // pure streaming read: workgroup b reads its contiguous 1/grid of the bytes, U x 16 B per lane in flight
 template <int U>
-__global__ void __launch_bounds__(1024) stream_kernel(const char* p, long long bytes, float* out) {
+__global__ void __launch_bounds__(1024) stream_kernel(const char* p, long long bytes, float* out,
+                                                      unsigned long long* st = nullptr) {
+    const unsigned long long t0 = st ? __builtin_amdgcn_s_memrealtime() : 0;
     const long long per = bytes / gridDim.x;
     const char* b = p + per * blockIdx.x;
     const int nvec = (int)(per / 16);
@@ -61,6 +63,15 @@ __global__ void __launch_bounds__(1024) stream_kernel(const char* p, long long b
         for (int j = 0; j < U; ++j) acc += __uint_as_float(w[j].x ^ w[j].y ^ w[j].z ^ w[j].w);
     }
     if (acc == 1.2345f) out[blockIdx.x] = acc;
+    if (st && (threadIdx.x & 63) == 0) {
+        unsigned long long* q = st + ((size_t)blockIdx.x * 16 + (threadIdx.x >> 6)) * 4;
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        q[0] = t0;
+        q[1] = t0 + 1000000000ull * (xcc & 15);  // xcc id folded into the staged slot (stream has no staging)
+        q[2] = __builtin_amdgcn_s_memrealtime();
+        q[3] = 1;
+    }
 }
 
 struct Shape {
@@ -78,6 +89,7 @@ struct Cfg {
 
 template <int R, int U, bool DB>
 static void run_cfg(const __half* W, const GemvIn& in, float* y, int rows, hipStream_t s) {
+    if (R == 0) return;
     EpiStore<R> e{y, nullptr, nullptr, 1.0f, rows};
     CK((launch_gemv<__half, R, U, true, false, DB>(W, in, e, (rows + R - 1) / R, s)));
 }
@@ -128,6 +140,93 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL(fill_f, dim3(64), dim3(256), 0, s, nw, 16384, 9u);
     CK(hipStreamSynchronize(s));
 
+    const std::string mode = argc > 1 ? argv[1] : "all";
+    auto in_for0 = [&](int si) { return GemvIn{x, si == 3 ? nullptr : nw, 1e-5f, kShapes[si].cols}; };
+    if (mode == "stamps") {
+        // per launch: first entry, staged/exit percentiles relative to it, and the gap to the next launch
+        const int nst = 256 * 16 * 4;
+        unsigned long long* st;
+        CK(hipMalloc(&st, (size_t)NL * nst * 8));
+        std::vector<unsigned long long> h((size_t)NL * nst);
+        auto report = [&](const char* name) {
+            CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+            double gap_sum = 0, dur_sum = 0;
+            std::vector<double> stg, ex;
+            for (int l = 2; l < NL; ++l) {
+                const unsigned long long* q = h.data() + (size_t)l * nst;
+                unsigned long long t0 = ~0ull, tl = 0;
+                for (int i = 0; i < 4096; ++i) {
+                    if (q[i * 4 + 3] == 0) continue;
+                    t0 = std::min(t0, q[i * 4]);
+                    tl = std::max(tl, q[i * 4 + 2]);
+                }
+                for (int i = 0; i < 4096; ++i) {
+                    if (q[i * 4 + 3] == 0) continue;
+                    stg.push_back((q[i * 4 + 1] - t0) * 0.01);
+                    ex.push_back((q[i * 4 + 2] - t0) * 0.01);
+                }
+                const unsigned long long* pq = h.data() + (size_t)(l - 1) * nst;
+                unsigned long long ptl = 0;
+                for (int i = 0; i < 4096; ++i)
+                    if (pq[i * 4 + 3]) ptl = std::max(ptl, pq[i * 4 + 2]);
+                gap_sum += (double)(t0 - ptl) * 0.01;
+                dur_sum += (double)(tl - t0) * 0.01;
+            }
+            std::sort(stg.begin(), stg.end());
+            std::sort(ex.begin(), ex.end());
+            auto pc = [](std::vector<double>& v, double f) { return v[(size_t)(f * (v.size() - 1))]; };
+            printf("%-16s in-kernel %6.2f us, gap before %5.2f us | staged p50 %5.2f p99 %5.2f | exit p10 %5.2f p50 %5.2f p90 %5.2f p100 %5.2f\n",
+                   name, dur_sum / (NL - 2), gap_sum / (NL - 2), pc(stg, .5), pc(stg, .99), pc(ex, .1), pc(ex, .5),
+                   pc(ex, .9), pc(ex, 1.0));
+        };
+        for (int si : {0, 1, 2, 3}) {
+            const Shape& sh = kShapes[si];
+            CK(hipMemset(st, 0, (size_t)NL * nst * 8));
+            time_graph(s, [&] {
+                for (int l = 0; l < NL; ++l)
+                    hipLaunchKernelGGL(stream_kernel<8>, dim3(256), dim3(1024), 0, s, (const char*)w[si][l],
+                                       (long long)sh.rows * sh.cols * 2, y2, st + (size_t)l * nst);
+            }, 1);
+            report((std::string(sh.name) + " stream").c_str());
+            {  // exit time by XCD (launches 2..NL-1), relative to each launch's first entry
+                double sum[8] = {0}, mx[8] = {0};
+                int cnt[8] = {0};
+                for (int l = 2; l < NL; ++l) {
+                    const unsigned long long* q = h.data() + (size_t)l * nst;
+                    unsigned long long t0 = ~0ull;
+                    for (int i = 0; i < 4096; ++i) t0 = std::min(t0, q[i * 4]);
+                    for (int i = 0; i < 4096; ++i) {
+                        const int xc = (int)((q[i * 4 + 1] - q[i * 4]) / 1000000000ull) & 7;
+                        const double e = (q[i * 4 + 2] - t0) * 0.01;
+                        sum[xc] += e;
+                        cnt[xc]++;
+                        mx[xc] = std::max(mx[xc], e);
+                    }
+                }
+                printf("   by XCD mean/max exit:");
+                for (int xc = 0; xc < 8; ++xc) printf(" %d:%.1f/%.1f", xc, cnt[xc] ? sum[xc] / cnt[xc] : 0.0, mx[xc]);
+                printf("\n");
+            }
+            for (int R : {1, 2}) {
+                CK(hipMemset(st, 0, (size_t)NL * nst * 8));
+                time_graph(s, [&] {
+                    for (int l = 0; l < NL; ++l) {
+                        GemvIn in = in_for0(si);
+                        in.stamps = st + (size_t)l * nst;
+                        if (R == 1) {
+                            EpiStore<1> e{y, nullptr, nullptr, 1.0f, sh.rows};
+                            CK((launch_gemv<__half, 1, 4, true, false, true>(w[si][l], in, e, sh.rows, s)));
+                        } else {
+                            EpiStore<2> e{y, nullptr, nullptr, 1.0f, sh.rows};
+                            CK((launch_gemv<__half, 2, 4, true, false, false>(w[si][l], in, e, sh.rows / 2, s)));
+                        }
+                    }
+                }, 1);
+                report((std::string(sh.name) + (R == 1 ? " R1U4DB" : " R2U4")).c_str());
+            }
+        }
+        return 0;
+    }
     std::vector<Cfg> cfgs = {
         {"R2U8", run_cfg<2, 8, false>},    {"R2U4 DB", run_cfg<2, 4, true>}, {"R1U8 DB", run_cfg<1, 8, true>},
         {"R1U8", run_cfg<1, 8, false>},    {"R1U16", run_cfg<1, 16, false>}, {"R2U4", run_cfg<2, 4, false>},
