@@ -52,6 +52,8 @@ struct AttnArgs {
     long long pos_stride;   // elements between positions
     long long head_stride;  // elements between kv heads
     float* part;            // [hq][max_splits][hd + kAttnPartPad]: o[hd], m, l, pad
+    float* out;             // [hq * hd] merged attention output
+    unsigned* counters;     // [n_kv_heads] arrival counters, zero between launches (the last arriver resets)
     const int32_t* pos_dev; // nullable: then pos_host
     int pos_host;
     int n_kv_heads;
@@ -185,6 +187,10 @@ __global__ void __launch_bounds__(64 * attn_waves(G)) attn_partial_kernel(AttnAr
         }
     }
     __syncthreads();
+    // Workgroup partial: the WAVES slice states merged in LDS, published write-through (sc1) so the
+    // head's last-arriving workgroup can read it from any XCD without a fence pair
+    // (MI355X_MICROARCH.md, hand-off table row 1: sc1 stores, drained, one agent-scope add per
+    // workgroup behind a workgroup barrier, sc1 loads by the last adder after the barrier it joins).
     for (int i = threadIdx.x; i < G * HD; i += blockDim.x) {
         const int g = i / HD, d = i - g * HD;
         float M = -INFINITY;
@@ -198,47 +204,48 @@ __global__ void __launch_bounds__(64 * attn_waves(G)) attn_partial_kernel(AttnAr
             L = fmaf(c, sh[w][g][HD + 1], L);
         }
         float* dst = a.part + ((size_t)(kvh * G + g) * a.max_splits + wgs) * (HD + kAttnPartPad);
-        dst[d] = o;
+        __hip_atomic_store(dst + d, o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (d == 0) {
-            dst[HD] = M;
-            dst[HD + 1] = L;
+            __hip_atomic_store(dst + HD, M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(dst + HD + 1, L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-}
-
-// One workgroup per query head: merge the live workgroup partials (independent loads per split).
-template <int HD>
-__global__ void __launch_bounds__(256)
-    attn_combine_kernel(const float* __restrict__ part, float* __restrict__ out, const int32_t* pos_dev,
-                        int pos_host, int max_splits, int ppw_wg) {
-    __shared__ float sw[kAttnMaxWgSplits];
-    __shared__ float sL;
-    const int h = blockIdx.x;
-    const int tid = threadIdx.x;
-    const int pos = pos_dev ? *pos_dev : pos_host;
-    const int ns = pos / ppw_wg + 1;
-    constexpr int PS = HD + kAttnPartPad;
-    const float* ph = part + (size_t)h * max_splits * PS;
-    if (tid < 64) {
-        float mx = -INFINITY;
-        for (int i = tid; i < ns; i += 64) mx = fmaxf(mx, ph[(size_t)i * PS + HD]);
-        mx = wave_max(mx);
-        float L = 0.0f;
-        for (int i = tid; i < ns; i += 64) {
-            const float w = expf(ph[(size_t)i * PS + HD] - mx);
-            sw[i] = w;
-            L = fmaf(w, ph[(size_t)i * PS + HD + 1], L);
-        }
-        L = wave_sum(L);
-        if (tid == 0) sL = L;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before the arrival
+    __syncthreads();
+    __shared__ int last;
+    const int ns = min(pos / (WAVES * PPW) + 1, a.max_splits);  // live workgroups of this kv head
+    if (threadIdx.x == 0) {
+        const unsigned prev = __hip_atomic_fetch_add(a.counters + kvh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = prev == (unsigned)(ns - 1);
+        if (last) __hip_atomic_store(a.counters + kvh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
-    const float L = sL;
-    for (int d = tid; d < HD; d += blockDim.x) {
-        float o = 0.0f;
-#pragma unroll 8
-        for (int i = 0; i < ns; ++i) o = fmaf(sw[i], ph[(size_t)i * PS + d], o);
-        out[(size_t)h * HD + d] = o / L;
+    if (!last) return;
+    // Last arriver: merge the head's ns partials in split order (deterministic whatever the arrival
+    // order): M = max m_i, w_i = e^{m_i - M}, out = (sum_i w_i o_i) / (sum_i w_i l_i).
+    float* ml = &sh[0][0][0];  // reuse: [G][ns][2]
+    for (int i = threadIdx.x; i < G * ns; i += blockDim.x) {
+        const int g = i / ns, sp = i - g * ns;
+        const float* src = a.part + ((size_t)(kvh * G + g) * a.max_splits + sp) * (HD + kAttnPartPad);
+        ml[2 * i] = __hip_atomic_load(src + HD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ml[2 * i + 1] = __hip_atomic_load(src + HD + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < G * HD; i += blockDim.x) {
+        const int g = i / HD, d = i - g * HD;
+        const float* src = a.part + (size_t)(kvh * G + g) * a.max_splits * (HD + kAttnPartPad) + d;
+        const float* mlg = ml + 2 * g * ns;
+        float M = -INFINITY;
+        for (int sp = 0; sp < ns; ++sp) M = fmaxf(M, mlg[2 * sp]);
+        float o = 0.0f, L = 0.0f;
+        for (int sp = 0; sp < ns; ++sp) {
+            const float w = expf(mlg[2 * sp] - M);
+            const float ov = __hip_atomic_load(src + (size_t)sp * (HD + kAttnPartPad), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+            o = fmaf(w, ov, o);
+            L = fmaf(w, mlg[2 * sp + 1], L);
+        }
+        a.out[(size_t)(kvh * G + g) * HD + d] = o / L;
     }
 }
 

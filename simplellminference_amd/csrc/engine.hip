@@ -66,6 +66,7 @@ struct sli_model {
     void* vc = nullptr;
     float *x = nullptr, *xpart = nullptr, *q = nullptr, *attn = nullptr, *act = nullptr, *logits = nullptr;
     float* part = nullptr;
+    unsigned* attn_count = nullptr;
     float *sin_t = nullptr, *cos_t = nullptr;
     unsigned long long* keys = nullptr;
     sli::DevState* st = nullptr;
@@ -278,38 +279,22 @@ struct StepRecorder {
         KT* kc = (KT*)m->kc + (size_t)l * m->hkv * m->T * m->hd;
         KT* vc = (KT*)m->vc + (size_t)l * m->hkv * m->T * m->hd;
         EpiQKV<KT> e{m->q, kc, vc, w.qkv_s, &m->st->pos, m->sin_t, m->cos_t, m->hq, m->hkv, m->hd, m->T};
-        SLI_HIP((launch_gemv<WT, 2, 4, NT, false, false>((const WT*)w.qkv, in, e, (m->hq + 2 * m->hkv) * (m->hd / 2), m->stream)));
+        SLI_HIP((launch_gemv<WT, 2, 4, NT, false>((const WT*)w.qkv, in, e, (m->hq + 2 * m->hkv) * (m->hd / 2), m->stream)));
         return SLI_OK;
     }
-    static bool fused_combine_fits(const sli_model* m) {
-        const int ppw = attn_wg_positions(m->c.kv_dtype, m->hd);
-        const size_t ml = sizeof(float) * 2 * (size_t)m->hq * ((m->T + ppw - 1) / ppw);
-        return gemv_lds_bytes(m->hq * m->hd) + ml <= 65536;
-    }
-    static int gemv_wo(sli_model* m, int l, bool fused_combine = false) {
+    static int gemv_wo(sli_model* m, int l) {
         const LayerW& w = m->layers[l];
         const bool tp = m->partial;
         GemvIn in{m->attn, nullptr, 0.0f, m->hq * m->hd};
-        if (fused_combine) {  // merge the attention partials in the prologue (no combine launch)
-            const int ppw = attn_wg_positions(m->c.kv_dtype, m->hd);
-            in.part = m->part;
-            in.pos = &m->st->pos;
-            in.hd = m->hd;
-            in.ppw_wg = ppw;
-            in.max_splits = (m->T + ppw - 1) / ppw;
-        }
         EpiStore<1> e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, w.wo_s, 1.0f, m->D};
-        if (fused_combine)
-            SLI_HIP((launch_gemv<WT, 1, 4, NT, true, true>((const WT*)w.wo, in, e, m->D, m->stream)));
-        else
-            SLI_HIP((launch_gemv<WT, 1, 4, NT, false, true>((const WT*)w.wo, in, e, m->D, m->stream)));
+        SLI_HIP((launch_gemv<WT, 1, 4, NT, true>((const WT*)w.wo, in, e, m->D, m->stream)));
         return SLI_OK;
     }
     static int gemv_gu(sli_model* m, int l) {
         const LayerW& w = m->layers[l];
         GemvIn in{m->x, m->norms + (size_t)(2 * l + 1) * m->D, m->c.eps, m->D};
         EpiSwiGLU e{m->act, w.gu_s, m->Il, m->c.act_mode};
-        SLI_HIP((launch_gemv<WT, 2, 8, NT, false, false>((const WT*)w.gu, in, e, m->Il, m->stream)));
+        SLI_HIP((launch_gemv<WT, 2, 8, NT, false>((const WT*)w.gu, in, e, m->Il, m->stream)));
         return SLI_OK;
     }
     static int gemv_down(sli_model* m, int l) {
@@ -317,7 +302,7 @@ struct StepRecorder {
         const bool tp = m->partial;
         GemvIn in{m->act, nullptr, 0.0f, m->Il};
         EpiStore<1> e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, w.down_s, 1.0f, m->D};
-        SLI_HIP((launch_gemv<WT, 1, 8, NT, false, true>((const WT*)w.down, in, e, m->D, m->stream)));
+        SLI_HIP((launch_gemv<WT, 1, 8, NT, true>((const WT*)w.down, in, e, m->D, m->stream)));
         return SLI_OK;
     }
     static int lm_head_blocks(sli_model* m) { return gemv_blocks((m->v_n + 1) / 2); }
@@ -325,7 +310,7 @@ struct StepRecorder {
         GemvIn in{m->x, m->norms + (size_t)(2 * m->L) * m->D, m->c.eps, m->D};
         EpiLogits<2> e{m->logits, m->keys, m->emb_s ? m->emb_s + m->v_lo : nullptr, m->v_n, m->v_lo, 0ull};
         const WT* w = (const WT*)m->emb + (size_t)m->v_lo * m->D;
-        SLI_HIP((launch_gemv<WT, 2, 4, NT, false, false>(w, in, e, (m->v_n + 1) / 2, m->stream)));
+        SLI_HIP((launch_gemv<WT, 2, 4, NT, false>(w, in, e, (m->v_n + 1) / 2, m->stream)));
         return SLI_OK;
     }
     static int allreduce_x(sli_model* m) {
@@ -339,7 +324,6 @@ struct StepRecorder {
         hipStream_t s = m->stream;
         SLI_TRY(embedding_launch(0, &m->st->token, m->emb, m->c.w_dtype, m->emb_s, m->x, m->V, m->D, s));
         const long long ps = m->hd, hs = (long long)m->T * m->hd, ls = (long long)m->hkv * m->T * m->hd;
-        const bool fuse = fused_combine_fits(m);  // split merge inside the wo GEMV prologue
         for (int l = 0; l < m->L; ++l) {
             SLI_TRY(gemv_qkv(m, l));
             StreamPrefetch pf;
@@ -347,8 +331,8 @@ struct StepRecorder {
             pf.bytes = (long long)m->D * m->hq * m->hd * (long long)m->wbytes;
             pf.blocks = m->pf_attn_blocks;
             SLI_TRY(mha_launch<KT>(m->q, (const KT*)m->kc, (const KT*)m->vc, m->attn, l, 0, &m->st->pos, m->T, m->hd,
-                                   m->hq, m->hkv, ps, hs, ls, m->part, s, /*combine=*/!fuse, pf));
-            SLI_TRY(gemv_wo(m, l, fuse));
+                                   m->hq, m->hkv, ps, hs, ls, m->part, m->attn_count, s, pf));
+            SLI_TRY(gemv_wo(m, l));
             SLI_TRY(allreduce_x(m));
             SLI_TRY(gemv_gu(m, l));
             SLI_TRY(gemv_down(m, l));
@@ -537,7 +521,8 @@ int sli_model_create(const sli_model_config* cfg, const void* comm_id, sli_model
     A((void**)&m->attn, sizeof(float) * m->hq * hd);
     A((void**)&m->act, sizeof(float) * m->Il);
     A((void**)&m->logits, sizeof(float) * m->v_n);
-    A((void**)&m->part, mha_workspace_bytes(m->T, m->hq, hd));  // split-context partials
+    A((void**)&m->part, mha_part_bytes(m->T, m->hq, hd));  // split-context partials
+    A((void**)&m->attn_count, sizeof(unsigned) * m->hkv);   // per-kv-head arrival counters (kept zero)
     A((void**)&m->sin_t, sizeof(float) * (size_t)m->T * (hd / 2));
     A((void**)&m->cos_t, sizeof(float) * (size_t)m->T * (hd / 2));
     A((void**)&m->keys, sizeof(unsigned long long) * kGemvMaxBlocks);
@@ -552,6 +537,7 @@ int sli_model_create(const sli_model_config* cfg, const void* comm_id, sli_model
         hipMemcpy(m->cos_t, co.data(), co.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
         return bail(fail(SLI_ERR_HIP, "rope table upload"));
     if (hipMemset(m->prompt, 0, sizeof(int32_t) * (m->T + 1)) != hipSuccess ||
+        hipMemset(m->attn_count, 0, sizeof(unsigned) * m->hkv) != hipSuccess ||
         hipMemset(m->hist, 0, sizeof(int32_t) * (m->T + 1)) != hipSuccess)
         return bail(fail(SLI_ERR_HIP, "memset"));
     if ((rc = sli_model_reset(m)) != SLI_OK) return bail(rc);

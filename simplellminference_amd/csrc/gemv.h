@@ -11,8 +11,6 @@
 //     (plain store, residual add, RoPE + KV-cache write, SwiGLU, logits + argmax keys).
 // Grid-stride over units so a launch is sized to the chip, not to the matrix.
 #pragma once
-#include <type_traits>
-
 #include "common.h"
 
 namespace sli {
@@ -22,11 +20,6 @@ struct GemvIn {
     const float* norm_w;  // nullptr: plain; else fused RMSNorm weight [cols]
     float eps;
     int cols;
-    // Fused split-context merge (attention.h partials): when part != nullptr, x is not read; the staged
-    // input is x[h*hd + d] = sum_i e^{m_i - M} o_i[d] / sum_i e^{m_i - M} l_i over the live splits of head h.
-    const float* part = nullptr;   // [cols / hd][max_splits][hd + kAttnPartPad]
-    const int32_t* pos = nullptr;  // live splits = *pos / ppw_wg + 1
-    int hd = 0, max_splits = 0, ppw_wg = 0;
     unsigned long long* stamps = nullptr;  // diagnostic (tools/gemv_lab): per-wave s_memrealtime x4
 };
 
@@ -100,68 +93,6 @@ struct XStage {
     }
 };
 
-// Merge the attention partials straight into the staged x (replaces attn_combine_kernel and its launch):
-// x[h*hd + d] = sum_i e^{m_i - M} o_i[d] / sum_i e^{m_i - M} l_i over the live splits of head h, summed in
-// split order. issue(): this thread's 4 columns of every split's o row and one (m, l) pair of the
-// table; commit(): the (m, l) table through LDS, then the merge — no global access after issue(), so
-// the weight loads behind it keep an exact vmcnt. Host contract (gemv_combine_ok): cols <= 4 * threads,
-// live splits <= CH, heads * splits <= threads. LDS: staged x [cols], then the (m, l) table.
-struct CombineStage {
-    static constexpr int CH = 8;
-    float4 po[CH];
-    float2 ml0;
-    __device__ __forceinline__ static const float* row(const GemvIn& in, int h, int i) {
-        return in.part + ((size_t)h * in.max_splits + i) * (in.hd + kAttnPartPad);
-    }
-    __device__ __forceinline__ static int live(const GemvIn& in) { return min(*in.pos / in.ppw_wg + 1, in.max_splits); }
-    __device__ __forceinline__ void issue(const GemvIn& in) {
-        const int tid = threadIdx.x, ns = live(in);
-        const int n4 = in.cols >> 2, nml = (in.cols / in.hd) * ns;
-        const int c4 = min(tid, n4 - 1);
-        const int h0 = (c4 << 2) / in.hd, d0 = (c4 << 2) - h0 * in.hd;
-#pragma unroll
-        for (int j = 0; j < CH; ++j) po[j] = *reinterpret_cast<const float4*>(row(in, h0, min(j, ns - 1)) + d0);
-        const int k = min(tid, nml - 1), h = k / ns, i = k - h * ns;
-        ml0 = *reinterpret_cast<const float2*>(row(in, h, i) + in.hd);
-    }
-    __device__ __forceinline__ void commit(float* smem, const GemvIn& in) {
-        float* xs = smem + kGemvLdsHead;
-        const int tid = threadIdx.x, ns = live(in);
-        const int n4 = in.cols >> 2, nml = (in.cols / in.hd) * ns;
-        float2* mls = reinterpret_cast<float2*>(xs + in.cols);
-        if (tid < nml) mls[tid] = ml0;
-        __syncthreads();
-        if (tid < n4) {
-            const int h = (tid << 2) / in.hd;
-            const float2* ml = mls + h * ns;
-            float M = -INFINITY;
-            for (int i = 0; i < ns; ++i) M = fmaxf(M, ml[i].x);
-            float L = 0.0f;
-            float4 o = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-#pragma unroll
-            for (int j = 0; j < CH; ++j) {
-                if (j < ns) {
-                    const float w = expf(ml[j].x - M);
-                    o.x = fmaf(w, po[j].x, o.x);
-                    o.y = fmaf(w, po[j].y, o.y);
-                    o.z = fmaf(w, po[j].z, o.z);
-                    o.w = fmaf(w, po[j].w, o.w);
-                    L = fmaf(w, ml[j].y, L);
-                }
-            }
-            reinterpret_cast<float4*>(xs)[tid] = make_float4(o.x / L, o.y / L, o.z / L, o.w / L);
-        }
-    }
-};
-
-// Host check for the fused merge (CombineStage contract).
-inline bool gemv_combine_ok(int cols, int hd, int max_splits) {
-    return cols <= 4 * kGemvThreads && max_splits <= CombineStage::CH && (cols / hd) * max_splits <= kGemvThreads;
-}
-
-inline size_t gemv_combine_lds(const GemvIn& in) {
-    return sizeof(float2) * (size_t)(in.cols / in.hd) * in.max_splits;
-}
 
 // One-shot staging for callers that have nothing to overlap it with.
 __device__ __forceinline__ void gemv_stage_x(float* smem, const GemvIn& in) {
@@ -206,7 +137,7 @@ __device__ __forceinline__ int gemv_unit_begin(int gwave, int nunits, int total_
     return (int)(((unsigned)gwave * (unsigned)nunits) / (unsigned)total_waves);
 }
 
-// Result slots in LDS behind the staged x (and the combine table): R floats per unit of the workgroup.
+// Result slots in LDS behind the staged x: R floats per unit of the workgroup.
 inline size_t gemv_res_floats(int units, int grid, int R) {
     return (size_t)R * ((size_t)units / grid + 2);
 }
@@ -225,8 +156,7 @@ inline size_t gemv_res_floats(int units, int grid, int R) {
 // for the first weight chunk (staged 4-6 us into a 10-30 us launch). The epilogue (residual reads,
 // RoPE, K/V writes, logits) runs once per workgroup after the loop, one thread per unit.
 // Prologue order: input loads, first weight chunk, input commit + barrier (see XStage).
-// CMB: stage x by merging attention partials (CombineStage) instead of reading in.x.
-template <typename WT, int R, int U, bool NT, class Epi, bool CMB = false, bool DB = (R * U <= 8)>
+template <typename WT, int R, int U, bool NT, class Epi, bool DB = (R * U <= 8)>
 __global__ void __launch_bounds__(kGemvThreads) gemv_kernel(const WT* __restrict__ W, GemvIn in, Epi epi_in) {
     Epi epi = epi_in;  // mutable per-thread copy (EpiLogits keeps a running key)
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -248,11 +178,11 @@ __global__ void __launch_bounds__(kGemvThreads) gemv_kernel(const WT* __restrict
     const int ue = gemv_unit_begin((blockIdx.x + 1) * nwaves, nunits, total_waves);
     const int cpr = (nvec + CV - 1) / CV;  // chunks per row
     const int nsteps = (u_end - u_begin) * cpr;
-    float* res = smem + kGemvLdsHead + in.cols + (CMB ? 2 * (in.cols / max(in.hd, 1)) * in.max_splits : 0);
+    float* res = smem + kGemvLdsHead + in.cols;
 
     const unsigned long long t_entry = in.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
-    using Stage = typename std::conditional<CMB, CombineStage, XStage>::type;
-    Stage stage;
+    unsigned long long t_staged = 0;
+    XStage stage;
     stage.issue(in);
     __builtin_amdgcn_sched_barrier(0);  // keep every input load ahead of the weight loads
 
@@ -303,7 +233,7 @@ __global__ void __launch_bounds__(kGemvThreads) gemv_kernel(const WT* __restrict
     __builtin_amdgcn_sched_barrier(0);
     stage.commit(smem, in);
     __syncthreads();
-    const unsigned long long t_staged = in.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+    t_staged = in.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
     if constexpr (DB) {
         u32x4 wb[U][R];
         int k = 0;
@@ -530,12 +460,11 @@ inline int gemv_blocks(int units) {
     return b < kGemvMaxBlocks ? (b > 0 ? b : 1) : kGemvMaxBlocks;
 }
 
-template <typename WT, int R, int U, bool NT, bool CMB = false, bool DB = (R * U <= 8), class Epi>
+template <typename WT, int R, int U, bool NT, bool DB = (R * U <= 8), class Epi>
 hipError_t launch_gemv(const WT* W, const GemvIn& in, const Epi& epi, int units, hipStream_t s) {
     const int grid = gemv_blocks(units);
-    const size_t lds = gemv_lds_bytes(in.cols) + (CMB ? gemv_combine_lds(in) : 0) +
-                       sizeof(float) * gemv_res_floats(units, grid, R);
-    hipLaunchKernelGGL((gemv_kernel<WT, R, U, NT, Epi, CMB, DB>), dim3(grid), dim3(kGemvThreads), lds, s, W, in, epi);
+    const size_t lds = gemv_lds_bytes(in.cols) + sizeof(float) * gemv_res_floats(units, grid, R);
+    hipLaunchKernelGGL((gemv_kernel<WT, R, U, NT, Epi, DB>), dim3(grid), dim3(kGemvThreads), lds, s, W, in, epi);
     return hipGetLastError();
 }
 

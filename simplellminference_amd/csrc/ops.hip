@@ -163,13 +163,13 @@ int attn_wg_positions(int kv_dtype, int head_dim) {
 template <typename KT, int HD>
 static int mha_launch_hd(const float* q, const KT* kc, const KT* vc, float* out, int layer, int pos, const int32_t* pos_dev,
                          int T, int H, int Hkv, long long pos_stride, long long head_stride, long long layer_stride,
-                         float* part, bool combine, hipStream_t s, const StreamPrefetch& pf) {
+                         float* part, unsigned* counters, hipStream_t s, const StreamPrefetch& pf) {
     using Geo = AttnGeom<KT, HD>;
     constexpr int ppw_wg = Geo::PPWG;
     const int wg_splits = (T + ppw_wg - 1) / ppw_wg;
-    if (wg_splits > kAttnMaxWgSplits) return fail(SLI_ERR_SHAPE, "mha: context too long for the combine kernel");
-    AttnArgs<KT> a{q, kc + (long long)layer * layer_stride, vc + (long long)layer * layer_stride, pos_stride,
-                   head_stride, part, pos_dev, pos, Hkv, wg_splits, 1.0f / sqrtf((float)HD), pf};
+    if (wg_splits > kAttnMaxWgSplits) return fail(SLI_ERR_SHAPE, "mha: context too long for the split merge");
+    AttnArgs<KT> a{q,    kc + (long long)layer * layer_stride, vc + (long long)layer * layer_stride, pos_stride,
+                   head_stride, part, out, counters, pos_dev, pos, Hkv, wg_splits, 1.0f / sqrtf((float)HD), pf};
     if (pf.bytes < 16 * (long long)pf.blocks) a.pf.blocks = 0;
     const int blocks = Hkv * wg_splits + a.pf.blocks;
     const int g = H / Hkv;
@@ -181,38 +181,37 @@ static int mha_launch_hd(const float* q, const KT* kc, const KT* vc, float* out,
         default: return fail(SLI_ERR_SHAPE, "mha: heads per kv head must be 1, 2, 4 or 8");
     }
     SLI_HIP(hipGetLastError());
-    if (!combine) return SLI_OK;  // the consumer merges the partials itself (CombineStage)
-    hipLaunchKernelGGL((attn_combine_kernel<HD>), dim3(H), dim3(128), 0, s, part, out, pos_dev, pos, wg_splits,
-                       ppw_wg);
-    SLI_HIP(hipGetLastError());
     return SLI_OK;
 }
 
 template <typename KT>
 int mha_launch(const float* q, const KT* kc, const KT* vc, float* out, int layer, int pos, const int32_t* pos_dev,
                int T, int hd, int H, int Hkv, long long pos_stride, long long head_stride, long long layer_stride,
-               float* part, hipStream_t s, bool combine, const StreamPrefetch& pf) {
+               float* part, unsigned* counters, hipStream_t s, const StreamPrefetch& pf) {
     if (hd == 128)
         return mha_launch_hd<KT, 128>(q, kc, vc, out, layer, pos, pos_dev, T, H, Hkv, pos_stride, head_stride,
-                                      layer_stride, part, combine, s, pf);
+                                      layer_stride, part, counters, s, pf);
     if (hd == 64)
         return mha_launch_hd<KT, 64>(q, kc, vc, out, layer, pos, pos_dev, T, H, Hkv, pos_stride, head_stride,
-                                     layer_stride, part, combine, s, pf);
+                                     layer_stride, part, counters, s, pf);
     return fail(SLI_ERR_SHAPE, "mha: head_dim must be 64 or 128");
 }
 
 template int mha_launch<float>(const float*, const float*, const float*, float*, int, int, const int32_t*, int, int,
-                               int, int, long long, long long, long long, float*, hipStream_t, bool,
+                               int, int, long long, long long, long long, float*, unsigned*, hipStream_t,
                                const StreamPrefetch&);
 template int mha_launch<__half>(const float*, const __half*, const __half*, float*, int, int, const int32_t*, int,
-                                int, int, int, long long, long long, long long, float*, hipStream_t, bool,
+                                int, int, int, long long, long long, long long, float*, unsigned*, hipStream_t,
                                 const StreamPrefetch&);
 
-size_t mha_workspace_bytes(int T, int H, int hd) {
+size_t mha_part_bytes(int T, int H, int hd) {
     const int ppw_wg_min = attn_wg_positions(SLI_DT_F32, hd);
     const size_t splits = (size_t)((T + ppw_wg_min - 1) / ppw_wg_min);
-    return sizeof(float) * (size_t)H * splits * (size_t)(hd + kAttnPartPad);
+    return (sizeof(float) * (size_t)H * splits * (size_t)(hd + kAttnPartPad) + 255) & ~(size_t)255;
 }
+
+// split partials, then one arrival counter per kv head (<= H)
+size_t mha_workspace_bytes(int T, int H, int hd) { return mha_part_bytes(T, H, hd) + sizeof(unsigned) * (size_t)H; }
 
 int embedding_launch(int token, const int32_t* token_dev, const void* table, int dtype, const float* row_scale,
                      float* out, int vocab, int dim, hipStream_t s) {
@@ -303,13 +302,16 @@ int sli_mha(const float* q, const void* kcache, const void* vcache, int kv_dtype
               "sli_mha: workspace too small");
     const long long kv = (long long)n_kv_heads * head_dim;
     hipStream_t s = as_stream(stream);
+    unsigned* counters = (unsigned*)((char*)workspace + mha_part_bytes(max_seq_len, n_heads, head_dim));
+    SLI_HIP(hipMemsetAsync(counters, 0, sizeof(unsigned) * n_kv_heads, s));
     if (kv_dtype == SLI_DT_F32)
         return mha_launch<float>(q, (const float*)kcache, (const float*)vcache, out, layer, pos, nullptr, max_seq_len,
-                                 head_dim, n_heads, n_kv_heads, kv, head_dim, kv * max_seq_len, (float*)workspace, s);
+                                 head_dim, n_heads, n_kv_heads, kv, head_dim, kv * max_seq_len, (float*)workspace,
+                                 counters, s);
     if (kv_dtype == SLI_DT_F16)
         return mha_launch<__half>(q, (const __half*)kcache, (const __half*)vcache, out, layer, pos, nullptr,
                                   max_seq_len, head_dim, n_heads, n_kv_heads, kv, head_dim, kv * max_seq_len,
-                                  (float*)workspace, s);
+                                  (float*)workspace, counters, s);
     return fail(SLI_ERR_ARG, "sli_mha: bad kv dtype");
 }
 

@@ -91,7 +91,7 @@ template <int R, int U, bool DB>
 static void run_cfg(const __half* W, const GemvIn& in, float* y, int rows, hipStream_t s) {
     if (R == 0) return;
     EpiStore<R> e{y, nullptr, nullptr, 1.0f, rows};
-    CK((launch_gemv<__half, R, U, true, false, DB>(W, in, e, (rows + R - 1) / R, s)));
+    CK((launch_gemv<__half, R, U, true, DB>(W, in, e, (rows + R - 1) / R, s)));
 }
 
 static float time_graph(hipStream_t s, const std::function<void()>& body, int reps = 5) {
@@ -209,20 +209,26 @@ int main(int argc, char** argv) {
             }
             for (int R : {1, 2}) {
                 CK(hipMemset(st, 0, (size_t)NL * nst * 8));
+                if (R == 3) {  // R=1 with the cross-wave barrier after the input loads (flag in stamps[0])
+                    for (int l = 0; l < NL; ++l) {
+                        const unsigned long long one = 1;
+                        CK(hipMemcpy(st + (size_t)l * nst, &one, 8, hipMemcpyHostToDevice));
+                    }
+                }
                 time_graph(s, [&] {
                     for (int l = 0; l < NL; ++l) {
                         GemvIn in = in_for0(si);
                         in.stamps = st + (size_t)l * nst;
-                        if (R == 1) {
+                        if (R != 2) {
                             EpiStore<1> e{y, nullptr, nullptr, 1.0f, sh.rows};
-                            CK((launch_gemv<__half, 1, 4, true, false, true>(w[si][l], in, e, sh.rows, s)));
+                            CK((launch_gemv<__half, 1, 4, true, true>(w[si][l], in, e, sh.rows, s)));
                         } else {
                             EpiStore<2> e{y, nullptr, nullptr, 1.0f, sh.rows};
-                            CK((launch_gemv<__half, 2, 4, true, false, false>(w[si][l], in, e, sh.rows / 2, s)));
+                            CK((launch_gemv<__half, 2, 4, true, false>(w[si][l], in, e, sh.rows / 2, s)));
                         }
                     }
                 }, 1);
-                report((std::string(sh.name) + (R == 1 ? " R1U4DB" : " R2U4")).c_str());
+                report((std::string(sh.name) + (R == 1 ? " R1U4DB" : R == 2 ? " R2U4" : " R1U4DB+bar")).c_str());
             }
         }
         return 0;
