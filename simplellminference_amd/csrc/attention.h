@@ -16,34 +16,6 @@
 
 namespace sli {
 
-// A byte range that extra workgroups of a latency-bound launch pull into the Infinity Cache (and L2)
-// for the NEXT launch, which then streams it at cache speed: decode attention reads 1/12 of a layer's
-// bytes and leaves HBM under-used, and the wo weights it precedes do not depend on it.
-struct StreamPrefetch {
-    const char* p = nullptr;
-    long long bytes = 0;
-    int blocks = 0;  // extra 256-thread workgroups appended to the grid
-};
-
-// Workgroup `b` of `pf.blocks` reads its contiguous share with default-policy (allocating) 16-byte loads.
-__device__ __forceinline__ void stream_prefetch_block(const StreamPrefetch& pf, int b) {
-    constexpr int U = 8;
-    const long long per = ((pf.bytes / pf.blocks) + 15) & ~15ll;
-    const long long lo = per * b, hi = min(pf.bytes, lo + per);
-    unsigned sink = 0;
-    for (long long o = lo + (long long)threadIdx.x * 16; o < hi; o += (long long)U * blockDim.x * 16) {
-        u32x4 w[U];
-#pragma unroll
-        for (int j = 0; j < U; ++j) {
-            const long long a = min(o + (long long)j * blockDim.x * 16, hi - 16);
-            w[j] = *reinterpret_cast<const u32x4*>(pf.p + a);
-        }
-#pragma unroll
-        for (int j = 0; j < U; ++j) sink ^= w[j].x;
-    }
-    if (sink == 0x9e3779b9u && pf.blocks < 0) asm volatile("" ::"v"(sink));  // keep the loads
-}
-
 template <typename KT>
 struct AttnArgs {
     const float* q;         // [hq * hd]
@@ -59,7 +31,6 @@ struct AttnArgs {
     int n_kv_heads;
     int max_splits;
     float scale;            // 1/sqrt(hd) (mha_kernel.cpp:41)
-    StreamPrefetch pf;      // optional: workgroups past n_kv_heads * max_splits prefetch this range
 };
 
 // A workgroup covers kAttnSlots wave-instructions of K (and of V) per lane-row group: WAVES waves of
@@ -83,22 +54,20 @@ __host__ __device__ constexpr int attn_waves(int g) { return g <= 2 ? 16 : 4; }
 
 // grid: n_kv_heads * wg_splits workgroups; wave w of workgroup (kvh, s) owns the w-th slice of split s.
 // The WAVES slice states are merged in LDS, so one partial per (q head, workgroup) reaches the workspace.
+// The split work of workgroup (kvh, wgs): partial state published write-through, arrival counted.
+// Returns true in the head's last-arriving workgroup (which must then merge the head: attn_merge).
+// Every return is uniform over the workgroup.
 template <typename KT, int HD, int G>
-__global__ void __launch_bounds__(64 * attn_waves(G)) attn_partial_kernel(AttnArgs<KT> a) {
+__device__ __forceinline__ bool attn_publish(const AttnArgs<KT>& a, int kvh, int wgs) {
     using Geo = AttnGeom<KT, HD>;
     constexpr int WAVES = attn_waves(G), kAttnNit = kAttnSlots / WAVES;
     constexpr int EPV = Geo::EPV, LPR = Geo::LPR, RPI = Geo::RPI, PPW = kAttnNit * RPI;
     __shared__ float sh[WAVES][G][HD + 2];
+    __shared__ int last;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    if ((int)blockIdx.x >= a.n_kv_heads * a.max_splits) {
-        stream_prefetch_block(a.pf, (int)blockIdx.x - a.n_kv_heads * a.max_splits);
-        return;
-    }
-    const int kvh = blockIdx.x / a.max_splits;  // max_splits counts workgroup splits here
-    const int wgs = blockIdx.x - kvh * a.max_splits;
     const int pos = a.pos_dev ? *a.pos_dev : a.pos_host;
-    if (wgs * WAVES * PPW > pos) return;  // whole workgroup past the live context (uniform exit)
+    if (wgs * WAVES * PPW > pos) return false;  // whole workgroup past the live context (uniform exit)
     const int t0 = (wgs * WAVES + wave) * PPW;
     const bool live_wave = t0 <= pos;
     const int t_end = min(t0 + PPW, pos + 1);
@@ -212,7 +181,6 @@ __global__ void __launch_bounds__(64 * attn_waves(G)) attn_partial_kernel(AttnAr
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before the arrival
     __syncthreads();
-    __shared__ int last;
     const int ns = min(pos / (WAVES * PPW) + 1, a.max_splits);  // live workgroups of this kv head
     if (threadIdx.x == 0) {
         const unsigned prev = __hip_atomic_fetch_add(a.counters + kvh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -220,33 +188,83 @@ __global__ void __launch_bounds__(64 * attn_waves(G)) attn_partial_kernel(AttnAr
         if (last) __hip_atomic_store(a.counters + kvh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
-    if (!last) return;
-    // Last arriver: merge the head's ns partials in split order (deterministic whatever the arrival
-    // order): M = max m_i, w_i = e^{m_i - M}, out = (sum_i w_i o_i) / (sum_i w_i l_i).
-    float* ml = &sh[0][0][0];  // reuse: [G][ns][2]
-    for (int i = threadIdx.x; i < G * ns; i += blockDim.x) {
-        const int g = i / ns, sp = i - g * ns;
-        const float* src = a.part + ((size_t)(kvh * G + g) * a.max_splits + sp) * (HD + kAttnPartPad);
-        ml[2 * i] = __hip_atomic_load(src + HD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ml[2 * i + 1] = __hip_atomic_load(src + HD + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < G * HD; i += blockDim.x) {
+    return last != 0;
+}
+
+// sc1 (L2-coherent across XCDs, L1 bypassed) 4-byte load, counted by the compiler like any other load.
+__device__ __forceinline__ float load_sc1(const float* base, unsigned bytes, unsigned off) {
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, bytes, 0x00020000);
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 16 /* sc1 */));
+}
+
+// Merge kv head kvh's ns live split partials into out (sc1 stores), by threads [t0, t0 + nthr) of the
+// workgroup, one output (q head g, dim d) per thread per pass, in split order whatever the arrival
+// order: M = max m_i, w_i = e^{m_i - M}, out = (sum_i w_i o_i) / (sum_i w_i l_i). Up to NS splits every
+// load of a thread (its head's NS (m, l) pairs, its NS partial values) is issued in ONE batch: one
+// round trip to the write-through copies; more splits take two passes in batches of NS. Ends with
+// the storing threads drained; no barrier.
+template <int HD, int G, int NS = 16>
+__device__ __forceinline__ void attn_merge(const float* part, float* out, int kvh, int max_splits, int ns, int t0,
+                                           int nthr) {
+    constexpr int PS = HD + kAttnPartPad;
+    const unsigned bytes = (unsigned)(sizeof(float) * (size_t)G * max_splits * PS);
+    const float* base = part + (size_t)kvh * G * max_splits * PS;
+    for (int i = (int)threadIdx.x - t0; i >= 0 && i < G * HD; i += nthr) {
         const int g = i / HD, d = i - g * HD;
-        const float* src = a.part + (size_t)(kvh * G + g) * a.max_splits * (HD + kAttnPartPad) + d;
-        const float* mlg = ml + 2 * g * ns;
+        const unsigned row0 = (unsigned)(g * max_splits) * PS;
         float M = -INFINITY;
-        for (int sp = 0; sp < ns; ++sp) M = fmaxf(M, mlg[2 * sp]);
-        float o = 0.0f, L = 0.0f;
-        for (int sp = 0; sp < ns; ++sp) {
-            const float w = expf(mlg[2 * sp] - M);
-            const float ov = __hip_atomic_load(src + (size_t)sp * (HD + kAttnPartPad), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-            o = fmaf(w, ov, o);
-            L = fmaf(w, mlg[2 * sp + 1], L);
+        if (ns > NS) {  // first pass: the max alone
+            for (int s0 = 0; s0 < ns; s0 += NS) {
+                float mv[NS];
+#pragma unroll
+                for (int j = 0; j < NS; ++j)
+                    mv[j] = load_sc1(base, bytes, 4u * (row0 + (unsigned)min(s0 + j, ns - 1) * PS + HD));
+#pragma unroll
+                for (int j = 0; j < NS; ++j) M = fmaxf(M, mv[j]);
+            }
         }
-        a.out[(size_t)(kvh * G + g) * HD + d] = o / L;
+        float o = 0.0f, L = 0.0f;
+        for (int s0 = 0; s0 < ns; s0 += NS) {
+            float mv[NS], lv[NS], ov[NS];
+#pragma unroll
+            for (int j = 0; j < NS; ++j) {
+                const unsigned r = row0 + (unsigned)min(s0 + j, ns - 1) * PS;
+                mv[j] = load_sc1(base, bytes, 4u * (r + HD));
+                lv[j] = load_sc1(base, bytes, 4u * (r + HD + 1));
+                ov[j] = load_sc1(base, bytes, 4u * (r + d));
+            }
+            if (ns <= NS) {
+#pragma unroll
+                for (int j = 0; j < NS; ++j) M = fmaxf(M, mv[j]);  // clamped duplicates leave the max
+            }
+#pragma unroll
+            for (int j = 0; j < NS; ++j) {
+                if (s0 + j < ns) {
+                    const float w = expf(mv[j] - M);
+                    o = fmaf(w, ov[j], o);
+                    L = fmaf(w, lv[j], L);
+                }
+            }
+        }
+        __hip_atomic_store(out + (size_t)(kvh * G + g) * HD + d, o / L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// Live split count of a kv head at position pos (workgroups that run attn_publish to the end).
+template <typename KT, int HD, int G>
+__device__ __forceinline__ int attn_live_splits(const AttnArgs<KT>& a) {
+    constexpr int PPWG = AttnGeom<KT, HD>::PPWG;
+    const int pos = a.pos_dev ? *a.pos_dev : a.pos_host;
+    return min(pos / PPWG + 1, a.max_splits);
+}
+
+// grid: n_kv_heads * wg_splits workgroups of 64 * attn_waves(G) threads
+template <typename KT, int HD, int G>
+__global__ void __launch_bounds__(64 * attn_waves(G)) attn_partial_kernel(AttnArgs<KT> a) {
+    const int kvh = blockIdx.x / a.max_splits;  // max_splits counts workgroup splits here
+    if (attn_publish<KT, HD, G>(a, kvh, blockIdx.x - kvh * a.max_splits))
+        attn_merge<HD, G>(a.part, a.out, kvh, a.max_splits, attn_live_splits<KT, HD, G>(a), 0, blockDim.x);
 }
 
 }  // namespace sli

@@ -52,7 +52,6 @@ struct sli_model {
     ncclComm_t comm = nullptr;
     bool partial = false;    // wo/down write per-rank partials (+ residual on rank 0) into xpart
     bool collectives = false;  // all-reduce partials / argmax keys over RCCL inside the step
-    int pf_attn_blocks = 0;    // extra attention workgroups that pull the layer's wo weights into the caches
     // local (this rank's) geometry
     int D = 0, L = 0, T = 0, V = 0, hd = 0, hq = 0, hkv = 0, Il = 0;
     int v_lo = 0, v_n = 0;
@@ -279,7 +278,7 @@ struct StepRecorder {
         KT* kc = (KT*)m->kc + (size_t)l * m->hkv * m->T * m->hd;
         KT* vc = (KT*)m->vc + (size_t)l * m->hkv * m->T * m->hd;
         EpiQKV<KT> e{m->q, kc, vc, w.qkv_s, &m->st->pos, m->sin_t, m->cos_t, m->hq, m->hkv, m->hd, m->T};
-        SLI_HIP((launch_gemv<WT, 2, 4, NT, false>((const WT*)w.qkv, in, e, (m->hq + 2 * m->hkv) * (m->hd / 2), m->stream)));
+        SLI_HIP((launch_gemv<WT, 2, 4, NT>((const WT*)w.qkv, in, e, (m->hq + 2 * m->hkv) * (m->hd / 2), m->stream)));
         return SLI_OK;
     }
     static int gemv_wo(sli_model* m, int l) {
@@ -287,14 +286,14 @@ struct StepRecorder {
         const bool tp = m->partial;
         GemvIn in{m->attn, nullptr, 0.0f, m->hq * m->hd};
         EpiStore<1> e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, w.wo_s, 1.0f, m->D};
-        SLI_HIP((launch_gemv<WT, 1, 4, NT, true>((const WT*)w.wo, in, e, m->D, m->stream)));
+        SLI_HIP((launch_gemv<WT, 1, 2, NT>((const WT*)w.wo, in, e, m->D, m->stream)));
         return SLI_OK;
     }
     static int gemv_gu(sli_model* m, int l) {
         const LayerW& w = m->layers[l];
         GemvIn in{m->x, m->norms + (size_t)(2 * l + 1) * m->D, m->c.eps, m->D};
         EpiSwiGLU e{m->act, w.gu_s, m->Il, m->c.act_mode};
-        SLI_HIP((launch_gemv<WT, 2, 8, NT, false>((const WT*)w.gu, in, e, m->Il, m->stream)));
+        SLI_HIP((launch_gemv<WT, 2, 4, NT>((const WT*)w.gu, in, e, m->Il, m->stream)));
         return SLI_OK;
     }
     static int gemv_down(sli_model* m, int l) {
@@ -302,7 +301,7 @@ struct StepRecorder {
         const bool tp = m->partial;
         GemvIn in{m->act, nullptr, 0.0f, m->Il};
         EpiStore<1> e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, w.down_s, 1.0f, m->D};
-        SLI_HIP((launch_gemv<WT, 1, 8, NT, true>((const WT*)w.down, in, e, m->D, m->stream)));
+        SLI_HIP((launch_gemv<WT, 1, 6, NT>((const WT*)w.down, in, e, m->D, m->stream)));
         return SLI_OK;
     }
     static int lm_head_blocks(sli_model* m) { return gemv_blocks((m->v_n + 1) / 2); }
@@ -310,7 +309,7 @@ struct StepRecorder {
         GemvIn in{m->x, m->norms + (size_t)(2 * m->L) * m->D, m->c.eps, m->D};
         EpiLogits<2> e{m->logits, m->keys, m->emb_s ? m->emb_s + m->v_lo : nullptr, m->v_n, m->v_lo, 0ull};
         const WT* w = (const WT*)m->emb + (size_t)m->v_lo * m->D;
-        SLI_HIP((launch_gemv<WT, 2, 4, NT, false>(w, in, e, (m->v_n + 1) / 2, m->stream)));
+        SLI_HIP((launch_gemv<WT, 2, 4, NT>(w, in, e, (m->v_n + 1) / 2, m->stream)));
         return SLI_OK;
     }
     static int allreduce_x(sli_model* m) {
@@ -326,12 +325,8 @@ struct StepRecorder {
         const long long ps = m->hd, hs = (long long)m->T * m->hd, ls = (long long)m->hkv * m->T * m->hd;
         for (int l = 0; l < m->L; ++l) {
             SLI_TRY(gemv_qkv(m, l));
-            StreamPrefetch pf;
-            pf.p = (const char*)m->layers[l].wo;
-            pf.bytes = (long long)m->D * m->hq * m->hd * (long long)m->wbytes;
-            pf.blocks = m->pf_attn_blocks;
             SLI_TRY(mha_launch<KT>(m->q, (const KT*)m->kc, (const KT*)m->vc, m->attn, l, 0, &m->st->pos, m->T, m->hd,
-                                   m->hq, m->hkv, ps, hs, ls, m->part, m->attn_count, s, pf));
+                                   m->hq, m->hkv, ps, hs, ls, m->part, m->attn_count, s));
             SLI_TRY(gemv_wo(m, l));
             SLI_TRY(allreduce_x(m));
             SLI_TRY(gemv_gu(m, l));
@@ -523,6 +518,7 @@ int sli_model_create(const sli_model_config* cfg, const void* comm_id, sli_model
     A((void**)&m->logits, sizeof(float) * m->v_n);
     A((void**)&m->part, mha_part_bytes(m->T, m->hq, hd));  // split-context partials
     A((void**)&m->attn_count, sizeof(unsigned) * m->hkv);   // per-kv-head arrival counters (kept zero)
+
     A((void**)&m->sin_t, sizeof(float) * (size_t)m->T * (hd / 2));
     A((void**)&m->cos_t, sizeof(float) * (size_t)m->T * (hd / 2));
     A((void**)&m->keys, sizeof(unsigned long long) * kGemvMaxBlocks);
@@ -549,11 +545,6 @@ int sli_model_create(const sli_model_config* cfg, const void* comm_id, sli_model
     const bool no_comm = c.tp_size > 1 && std::getenv("SLI_DEBUG_NOCOMM") != nullptr;
     m->partial = c.tp_size > 1 || force_comm;
     m->collectives = (c.tp_size > 1 && !no_comm) || force_comm;
-    {  // attention-side prefetch of the wo weights (workgroups appended to the attention grid)
-        const char* pf = std::getenv("SLI_PF_ATTN");
-        m->pf_attn_blocks = pf ? std::atoi(pf) : 0;
-    }
-
     if (m->collectives) {
         ncclUniqueId id;
         if (comm_id) {

@@ -144,7 +144,7 @@ inline size_t gemv_res_floats(int units, int grid, int R) {
 
 // Wave-level schedule. Wave gw of the grid owns units [gw*N/W, (gw+1)*N/W) (balanced: sizes differ by at
 // most one); a unit is R rows chosen by the epilogue, streamed in chunks of U 16-byte vectors per row
-// per lane. The wave's work is the flat sequence of (unit, chunk) steps; with DB the next step's loads
+// per lane. The wave's work is the flat sequence of (unit, chunk) steps; the next step's loads
 // are issued before the current step is consumed (two register buffers), so each wave keeps a chunk in
 // flight while it computes.
 //
@@ -156,10 +156,9 @@ inline size_t gemv_res_floats(int units, int grid, int R) {
 // for the first weight chunk (staged 4-6 us into a 10-30 us launch). The epilogue (residual reads,
 // RoPE, K/V writes, logits) runs once per workgroup after the loop, one thread per unit.
 // Prologue order: input loads, first weight chunk, input commit + barrier (see XStage).
-template <typename WT, int R, int U, bool NT, class Epi, bool DB = (R * U <= 8)>
-__global__ void __launch_bounds__(kGemvThreads) gemv_kernel(const WT* __restrict__ W, GemvIn in, Epi epi_in) {
-    Epi epi = epi_in;  // mutable per-thread copy (EpiLogits keeps a running key)
-    extern __shared__ __attribute__((aligned(16))) float smem[];
+template <typename WT, int R, int U, bool NT, class Epi, class Stage>
+__device__ __forceinline__ void gemv_block(const WT* __restrict__ W, const GemvIn& in, Epi& epi, Stage& stage,
+                                           float* smem) {
     const float* xs = smem + kGemvLdsHead;
 
     constexpr int EPV = Vec16<WT>::N;
@@ -182,7 +181,6 @@ __global__ void __launch_bounds__(kGemvThreads) gemv_kernel(const WT* __restrict
 
     const unsigned long long t_entry = in.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
     unsigned long long t_staged = 0;
-    XStage stage;
     stage.issue(in);
     __builtin_amdgcn_sched_barrier(0);  // keep every input load ahead of the weight loads
 
@@ -225,38 +223,36 @@ __global__ void __launch_bounds__(kGemvThreads) gemv_kernel(const WT* __restrict
         }
     };
 
-    u32x4 wa[U][R];
+    // Two register buffers, both in flight before the input is committed. Every load is unconditional:
+    // a position past the wave's last step is clamped to that step, so the extra load duplicates one
+    // issued just before it (an in-flight miss to the same lines) and is never consumed; no clamped load
+    // is ever issued after its data was consumed (a fresh HBM round trip at the end of every wave).
+    u32x4 wa[U][R], wb[U][R];
     int lu = u_begin, lc = 0;  // next step to load
     int cu = u_begin, cc = 0;  // next step to consume
     load_step(lu, lc, wa);
+    next(lu, lc);
+    load_step(lu, lc, wb);
     next(lu, lc);
     __builtin_amdgcn_sched_barrier(0);
     stage.commit(smem, in);
     __syncthreads();
     t_staged = in.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
-    if constexpr (DB) {
-        u32x4 wb[U][R];
-        int k = 0;
-        for (; k + 1 < nsteps; k += 2) {
-            load_step(lu, lc, wb);
-            next(lu, lc);
-            consume_step(cu, cc, wa);
-            next(cu, cc);
-            load_step(lu, lc, wa);  // past the end: a clamped re-read, never consumed
-            next(lu, lc);
-            consume_step(cu, cc, wb);
-            next(cu, cc);
-        }
-        if (k < nsteps) consume_step(cu, cc, wa);
-    } else {
-        for (int k = 0; k < nsteps; ++k) {
-            if (k > 0) {
-                load_step(lu, lc, wa);
-                next(lu, lc);
-            }
-            consume_step(cu, cc, wa);
-            next(cu, cc);
-        }
+    int k = 0;
+    for (; k + 2 < nsteps; k += 2) {
+        consume_step(cu, cc, wa);
+        next(cu, cc);
+        load_step(lu, lc, wa);  // step k + 2
+        next(lu, lc);
+        consume_step(cu, cc, wb);
+        next(cu, cc);
+        load_step(lu, lc, wb);  // step k + 3, or a duplicate of k + 2
+        next(lu, lc);
+    }
+    if (k < nsteps) {
+        consume_step(cu, cc, wa);
+        next(cu, cc);
+        if (k + 1 < nsteps) consume_step(cu, cc, wb);
     }
     __syncthreads();
     for (int u = ub + (int)threadIdx.x; u < ue; u += blockDim.x) {
@@ -272,6 +268,14 @@ __global__ void __launch_bounds__(kGemvThreads) gemv_kernel(const WT* __restrict
         p[2] = __builtin_amdgcn_s_memrealtime();
         p[3] = (unsigned long long)max(nsteps, 1);
     }
+}
+
+template <typename WT, int R, int U, bool NT, class Epi>
+__global__ void __launch_bounds__(kGemvThreads) gemv_kernel(const WT* __restrict__ W, GemvIn in, Epi epi_in) {
+    Epi epi = epi_in;  // mutable per-thread copy (EpiLogits keeps a running key)
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    XStage stage;
+    gemv_block<WT, R, U, NT>(W, in, epi, stage, smem);
 }
 
 // Row-by-row fallback for shapes the vector kernel cannot take (cols*sizeof(WT) not a multiple of 16
@@ -460,11 +464,11 @@ inline int gemv_blocks(int units) {
     return b < kGemvMaxBlocks ? (b > 0 ? b : 1) : kGemvMaxBlocks;
 }
 
-template <typename WT, int R, int U, bool NT, bool DB = (R * U <= 8), class Epi>
+template <typename WT, int R, int U, bool NT, class Epi>
 hipError_t launch_gemv(const WT* W, const GemvIn& in, const Epi& epi, int units, hipStream_t s) {
     const int grid = gemv_blocks(units);
     const size_t lds = gemv_lds_bytes(in.cols) + sizeof(float) * gemv_res_floats(units, grid, R);
-    hipLaunchKernelGGL((gemv_kernel<WT, R, U, NT, Epi, DB>), dim3(grid), dim3(kGemvThreads), lds, s, W, in, epi);
+    hipLaunchKernelGGL((gemv_kernel<WT, R, U, NT, Epi>), dim3(grid), dim3(kGemvThreads), lds, s, W, in, epi);
     return hipGetLastError();
 }
 

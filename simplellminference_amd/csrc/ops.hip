@@ -144,8 +144,7 @@ static int matmul_dispatch(const float* x, const WT* w, const float* rscale, flo
     if (vec_ok) {
         EpiStore<2> epi{y, nullptr, rscale, scale, rows};
         GemvIn in{x, nullptr, 0.0f, cols};
-        constexpr int U = sizeof(WT) == 1 ? 4 : 8;
-        SLI_HIP((launch_gemv<WT, 2, U, true>(w, in, epi, (rows + 1) / 2, s)));
+        SLI_HIP((launch_gemv<WT, 2, 4, true>(w, in, epi, (rows + 1) / 2, s)));
     } else {
         const int blocks = std::min(kGemvMaxBlocks, (rows + 3) / 4);
         hipLaunchKernelGGL(gemv_scalar_kernel<WT>, dim3(blocks), dim3(kGemvThreads), 0, s, w, x, rscale, y, rows,
@@ -163,15 +162,14 @@ int attn_wg_positions(int kv_dtype, int head_dim) {
 template <typename KT, int HD>
 static int mha_launch_hd(const float* q, const KT* kc, const KT* vc, float* out, int layer, int pos, const int32_t* pos_dev,
                          int T, int H, int Hkv, long long pos_stride, long long head_stride, long long layer_stride,
-                         float* part, unsigned* counters, hipStream_t s, const StreamPrefetch& pf) {
+                         float* part, unsigned* counters, hipStream_t s) {
     using Geo = AttnGeom<KT, HD>;
     constexpr int ppw_wg = Geo::PPWG;
     const int wg_splits = (T + ppw_wg - 1) / ppw_wg;
     if (wg_splits > kAttnMaxWgSplits) return fail(SLI_ERR_SHAPE, "mha: context too long for the split merge");
     AttnArgs<KT> a{q,    kc + (long long)layer * layer_stride, vc + (long long)layer * layer_stride, pos_stride,
-                   head_stride, part, out, counters, pos_dev, pos, Hkv, wg_splits, 1.0f / sqrtf((float)HD), pf};
-    if (pf.bytes < 16 * (long long)pf.blocks) a.pf.blocks = 0;
-    const int blocks = Hkv * wg_splits + a.pf.blocks;
+                   head_stride, part, out, counters, pos_dev, pos, Hkv, wg_splits, 1.0f / sqrtf((float)HD)};
+    const int blocks = Hkv * wg_splits;
     const int g = H / Hkv;
     switch (g) {
         case 1: hipLaunchKernelGGL((attn_partial_kernel<KT, HD, 1>), dim3(blocks), dim3(64 * attn_waves(1)), 0, s, a); break;
@@ -187,22 +185,20 @@ static int mha_launch_hd(const float* q, const KT* kc, const KT* vc, float* out,
 template <typename KT>
 int mha_launch(const float* q, const KT* kc, const KT* vc, float* out, int layer, int pos, const int32_t* pos_dev,
                int T, int hd, int H, int Hkv, long long pos_stride, long long head_stride, long long layer_stride,
-               float* part, unsigned* counters, hipStream_t s, const StreamPrefetch& pf) {
+               float* part, unsigned* counters, hipStream_t s) {
     if (hd == 128)
         return mha_launch_hd<KT, 128>(q, kc, vc, out, layer, pos, pos_dev, T, H, Hkv, pos_stride, head_stride,
-                                      layer_stride, part, counters, s, pf);
+                                      layer_stride, part, counters, s);
     if (hd == 64)
         return mha_launch_hd<KT, 64>(q, kc, vc, out, layer, pos, pos_dev, T, H, Hkv, pos_stride, head_stride,
-                                     layer_stride, part, counters, s, pf);
+                                     layer_stride, part, counters, s);
     return fail(SLI_ERR_SHAPE, "mha: head_dim must be 64 or 128");
 }
 
 template int mha_launch<float>(const float*, const float*, const float*, float*, int, int, const int32_t*, int, int,
-                               int, int, long long, long long, long long, float*, unsigned*, hipStream_t,
-                               const StreamPrefetch&);
+                               int, int, long long, long long, long long, float*, unsigned*, hipStream_t);
 template int mha_launch<__half>(const float*, const __half*, const __half*, float*, int, int, const int32_t*, int,
-                                int, int, int, long long, long long, long long, float*, unsigned*, hipStream_t,
-                                const StreamPrefetch&);
+                                int, int, int, long long, long long, long long, float*, unsigned*, hipStream_t);
 
 size_t mha_part_bytes(int T, int H, int hd) {
     const int ppw_wg_min = attn_wg_positions(SLI_DT_F32, hd);

@@ -74,6 +74,38 @@ __global__ void __launch_bounds__(1024) stream_kernel(const char* p, long long b
     }
 }
 
+// latency probe: wave 0 times one L2-hot load while the other 15 waves of the CU have `nw` 16-byte HBM
+// loads per lane in flight (nw = 0: idle CU). scalar = 1: wave 0 uses a scalar (s_load) read instead.
+__global__ void __launch_bounds__(1024) probe_kernel(const char* W, const float* x, int nw, int scalar,
+                                                     unsigned long long* out, float* sink) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float acc = 0.0f;
+    if (wave > 0) {
+        const char* b = W + ((size_t)blockIdx.x * 16 + wave) * 16384;  // 16 KiB per wave: 64 MiB in all
+        u32x4 w[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+            if (j < nw) w[j] = load16<true>(b + (size_t)(j * 64 + lane) * 16);
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+            if (j < nw) acc += __uint_as_float(w[j].x);
+    } else {
+        __builtin_amdgcn_s_sleep(20);  // let the other waves issue first
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        float v;
+        if (scalar) {
+            v = __builtin_nontemporal_load(x + 7);  // uniform address
+        } else {
+            v = x[lane];
+        }
+        acc = v;
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) out[blockIdx.x] = t1 - t0;
+    }
+    if (acc == 1.2345f) sink[threadIdx.x] = acc;
+}
+
 struct Shape {
     const char* name;
     int rows, cols;
@@ -91,7 +123,7 @@ template <int R, int U, bool DB>
 static void run_cfg(const __half* W, const GemvIn& in, float* y, int rows, hipStream_t s) {
     if (R == 0) return;
     EpiStore<R> e{y, nullptr, nullptr, 1.0f, rows};
-    CK((launch_gemv<__half, R, U, true, DB>(W, in, e, (rows + R - 1) / R, s)));
+    CK((launch_gemv<__half, R, U, true>(W, in, e, (rows + R - 1) / R, s)));
 }
 
 static float time_graph(hipStream_t s, const std::function<void()>& body, int reps = 5) {
@@ -142,6 +174,43 @@ int main(int argc, char** argv) {
 
     const std::string mode = argc > 1 ? argv[1] : "all";
     auto in_for0 = [&](int si) { return GemvIn{x, si == 3 ? nullptr : nw, 1e-5f, kShapes[si].cols}; };
+    if (mode == "mall") {
+        // wo GEMV (R1U2) timed cold (distinct layers) and right after a streaming read of the same matrix
+        // (Infinity-Cache hot): is a prefetch in an earlier launch worth anything to the GEMV?
+        const Shape& sh = kShapes[1];
+        const long long bytes = (long long)sh.rows * sh.cols * 2;
+        auto gemv = [&](int l) {
+            EpiStore<1> e{y, nullptr, nullptr, 1.0f, sh.rows};
+            CK((launch_gemv<__half, 1, 2, true>(w[1][l], in_for0(1), e, sh.rows, s)));
+        };
+        auto strm = [&](int l) {
+            hipLaunchKernelGGL(stream_kernel<8>, dim3(256), dim3(1024), 0, s, (const char*)w[1][l], bytes, y2, nullptr);
+        };
+        const float cold = time_graph(s, [&] { for (int l = 0; l < NL; ++l) gemv(l); });
+        const float str = time_graph(s, [&] { for (int l = 0; l < NL; ++l) strm(l); });
+        const float both = time_graph(s, [&] { for (int l = 0; l < NL; ++l) { strm(l); gemv(l); } });
+        const float both2 = time_graph(s, [&] { for (int l = 0; l < NL; ++l) { strm(l); strm(l); } });
+        printf("wo gemv cold %.2f us, stream cold %.2f us, stream+gemv(hot) %.2f us -> hot gemv ~%.2f us; stream+stream(hot) -> hot stream ~%.2f us\n",
+               1000 * cold / NL, 1000 * str / NL, 1000 * both / NL, 1000 * (both - str) / NL, 1000 * (both2 - str) / NL);
+        return 0;
+    }
+    if (mode == "probe") {
+        unsigned long long* o;
+        CK(hipMalloc(&o, 256 * 8));
+        std::vector<unsigned long long> h(256);
+        for (int sc : {0, 1})
+            for (int nwl : {0, 1, 4, 8, 16}) {
+                for (int rep = 0; rep < 3; ++rep) {
+                    hipLaunchKernelGGL(probe_kernel, dim3(256), dim3(1024), 0, s, (const char*)w[2][rep], x, nwl, sc, o, y2);
+                    CK(hipStreamSynchronize(s));
+                }
+                CK(hipMemcpy(h.data(), o, 256 * 8, hipMemcpyDeviceToHost));
+                std::sort(h.begin(), h.end());
+                printf("probe scalar=%d other waves' loads/lane=%2d: wave-0 load latency p50 %.2f us p90 %.2f max %.2f\n", sc,
+                       nwl, h[128] * 0.01, h[230] * 0.01, h[255] * 0.01);
+            }
+        return 0;
+    }
     if (mode == "stamps") {
         // per launch: first entry, staged/exit percentiles relative to it, and the gap to the next launch
         const int nst = 256 * 16 * 4;
@@ -221,10 +290,10 @@ int main(int argc, char** argv) {
                         in.stamps = st + (size_t)l * nst;
                         if (R != 2) {
                             EpiStore<1> e{y, nullptr, nullptr, 1.0f, sh.rows};
-                            CK((launch_gemv<__half, 1, 4, true, true>(w[si][l], in, e, sh.rows, s)));
+                            CK((launch_gemv<__half, 1, 4, true>(w[si][l], in, e, sh.rows, s)));
                         } else {
                             EpiStore<2> e{y, nullptr, nullptr, 1.0f, sh.rows};
-                            CK((launch_gemv<__half, 2, 4, true, false>(w[si][l], in, e, sh.rows / 2, s)));
+                            CK((launch_gemv<__half, 2, 4, true>(w[si][l], in, e, sh.rows / 2, s)));
                         }
                     }
                 }, 1);
@@ -234,9 +303,9 @@ int main(int argc, char** argv) {
         return 0;
     }
     std::vector<Cfg> cfgs = {
-        {"R2U8", run_cfg<2, 8, false>},    {"R2U4 DB", run_cfg<2, 4, true>}, {"R1U8 DB", run_cfg<1, 8, true>},
-        {"R1U8", run_cfg<1, 8, false>},    {"R1U16", run_cfg<1, 16, false>}, {"R2U4", run_cfg<2, 4, false>},
-        {"R1U4 DB", run_cfg<1, 4, true>},  {"R4U2 DB", run_cfg<4, 2, true>},
+        {"R2U4", run_cfg<2, 4, true>}, {"R1U8", run_cfg<1, 8, true>}, {"R1U4", run_cfg<1, 4, true>},
+        {"R4U2", run_cfg<4, 2, true>}, {"R2U2", run_cfg<2, 2, true>}, {"R1U2", run_cfg<1, 2, true>},
+        {"R1U6", run_cfg<1, 6, true>},
     };
     auto in_for = [&](int si) { return GemvIn{x, si == 3 ? nullptr : nw, 1e-5f, kShapes[si].cols}; };
 
@@ -293,7 +362,7 @@ int main(int argc, char** argv) {
                 }
         });
         const double us = 1000.0 * ms / NL;
-        printf("layer chain %s: %8.2f us/layer  %7.1f GB/s  [", pick ? "best" : "R2U8", us, lbytes / (us * 1e-6) / 1e9);
+        printf("layer chain %s: %8.2f us/layer  %7.1f GB/s  [", pick ? "best" : "R2U4", us, lbytes / (us * 1e-6) / 1e9);
         for (int si = 0; si < 4; ++si) printf(" %s=%s", kShapes[si].name, cfgs[pick ? best[si] : 0].name);
         printf(" ]\n");
     }
