@@ -1,0 +1,38 @@
+"""HBM traffic per GEMV launch from a rocprofv3 FETCH_SIZE pass (run tools/pmc_traffic.sh on the GPU box).
+
+FETCH_SIZE is in KiB and, on gfx950, reads exactly half the bytes of a wide coalesced 16-B/lane stream
+(cdna_hip_programming.md section 7; MI355X_MICROARCH.md HBM), so traffic = 2 * FETCH_SIZE * 1024. Only
+the decode step's own GEMV dispatches are counted: the weight-placement and KV-fill kernels at model
+build are skipped by name.
+    python tools/pmc_traffic.py <counter_collection.csv> <algorithmic bytes per launch> <out.json> <key>
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+path, alg, out, key = sys.argv[1], float(sys.argv[2]), sys.argv[3], sys.argv[4]
+per = defaultdict(list)
+for r in csv.DictReader(open(path)):
+    if r.get("Counter_Name") != "FETCH_SIZE":
+        continue
+    per[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+gemv = [v for k, vs in per.items() if "gemv_kernel" in k for v in vs]
+if not gemv:
+    raise SystemExit("no gemv_kernel dispatches with FETCH_SIZE in " + path)
+kb = sum(gemv) / len(gemv)
+res = {}
+try:
+    res = json.load(open(out))
+except (OSError, ValueError):
+    pass
+res[key] = {
+    "hbm_bytes_per_launch": round(2 * kb * 1024),
+    "fetch_size_kib_per_launch_raw": round(kb, 1),
+    "correction": "x2: gfx950 FETCH_SIZE counts half the bytes of a coalesced 16-B/lane stream",
+    "algorithmic_bytes_per_launch": round(alg),
+    "gemv_dispatches": len(gemv),
+    "per_kernel_mean_kib_raw": {k.split("(")[0][:90]: round(sum(v) / len(v), 1) for k, v in per.items() if "gemv" in k},
+}
+json.dump(res, open(out, "w"), indent=1)
+print(json.dumps(res[key], indent=1))
