@@ -64,6 +64,15 @@ int sli_stream_sync(sli_stream_t stream);
 int sli_matmul(const float* x, const void* w, int w_dtype, const float* w_row_scale, float* y, int32_t rows,
                int32_t cols, float scale, sli_stream_t stream);
 
+/* Batched projection for B sequences decoding in lockstep (the reference is batch 1; this serves
+ * SURVEY.md §8 config C4): y[b][r] = sum_c x[b][c] * W[r][c] for b < batch <= 8, on MFMA
+ * (v_mfma_f32_16x16x32_f16; the fp32 input is carried as fp16 hi + lo columns). x [batch][cols] fp32, W
+ * [rows][cols] fp16 (SLI_DT_F16 only), y [batch][rows] fp32, cols % 32 == 0. The workspace
+ * (sli_matmul_batch_workspace_bytes, 0 = unsupported shape) holds split-K partials and counters. */
+size_t sli_matmul_batch_workspace_bytes(int32_t rows, int32_t cols, int32_t batch);
+int sli_matmul_batch(const float* x, const void* w, int w_dtype, float* y, int32_t rows, int32_t cols, int32_t batch,
+                     void* workspace, size_t workspace_bytes, sli_stream_t stream);
+
 /* kernel::rmsnorm_kernel_cuda (rms_kernel.cuh:6-7; CPU rms_kernel.cpp:5-23): y = x / sqrt(mean(x^2)+eps) * w.
  * Single-workgroup reduction: no atomics, no per-call allocation (the reference allocates + memsets a
  * {1} tensor per call and races across blocks, rms_kernel.cu:29-33,48-51). */
@@ -117,6 +126,8 @@ typedef struct {
     int32_t act_mode; /* 0: reference sigmoid(gate)*up (swiglu_kernel.cpp:12-13); 1: SiLU(gate)*up */
     int32_t tp_rank, tp_size;
     int32_t device;
+    int32_t batch;    /* sequences decoding in lockstep, <= 8 (0 or 1: batch 1, the reference's case).
+                         batch > 1 runs the projections on MFMA (sli_matmul_batch) and needs fp16 weights */
 } sli_model_config;
 
 typedef struct sli_model sli_model;
@@ -147,7 +158,8 @@ int sli_model_set_weight(sli_model* m, int32_t kind, int32_t index, const float*
 int sli_model_load_flat(sli_model* m, const char* path);
 /* Zero the KV cache and the decode state. */
 int sli_model_reset(sli_model* m);
-/* Fill K/V rows [0, upto) of every layer with the synthetic N(0,1) values (bench context fill). */
+/* Fill K/V rows [0, upto) of every layer with the synthetic N(0,1) values (bench context fill); sequence b
+ * of a batch uses seed + b. */
 int sli_model_fill_kv_synthetic(sli_model* m, uint32_t seed, int32_t upto);
 /* Decode state: the token fed at position pos. advance=1: after each step pos += 1 and the next token
  * is the teacher-forced prompt id or the greedy argmax (model.cpp:157-183); advance=0: the step is
@@ -155,18 +167,32 @@ int sli_model_fill_kv_synthetic(sli_model* m, uint32_t seed, int32_t upto);
 int sli_model_set_state(sli_model* m, int32_t token, int32_t pos, int32_t advance);
 int sli_model_set_prompt(sli_model* m, const int32_t* ids, int32_t n);
 int sli_model_get_state(sli_model* m, int32_t* pos, int32_t* token, int32_t* last_argmax, int32_t* error);
+/* Per-sequence forms for batch > 1 (seq < batch). The sequence-less setters above act on every sequence,
+ * the getters on sequence 0. */
+int sli_model_set_state_seq(sli_model* m, int32_t seq, int32_t token, int32_t pos, int32_t advance);
+int sli_model_set_prompt_seq(sli_model* m, int32_t seq, const int32_t* ids, int32_t n);
+int sli_model_get_state_seq(sli_model* m, int32_t seq, int32_t* pos, int32_t* token, int32_t* last_argmax,
+                            int32_t* error);
+/* The tokens fed at positions [0, n) of sequence seq. */
+int sli_model_get_history(sli_model* m, int32_t seq, int32_t n, int32_t* out);
 /* One decode step (hipGraph replay; captured on first use). Asynchronous on the model's stream. */
 int sli_model_step(sli_model* m);
 int sli_model_sync(sli_model* m);
-/* logits of the last step: this rank's vocab shard [vocab_lo, vocab_lo+n). */
+/* logits of the last step: this rank's vocab shard [vocab_lo, vocab_lo+n) of every sequence, [batch][n]. */
 int sli_model_get_logits(sli_model* m, float* host, int32_t n, int32_t* vocab_lo);
 /* LlamaModel::predict on token ids: tokens_out[t] = token fed at position t; logits_out optional
- * [max_length][local vocab]. */
+ * [max_length][local vocab]. batch > 1: every sequence gets the prompt, tokens_out is [batch][max_length]
+ * and logits_out [max_length][batch][local vocab]. */
 int sli_model_predict(sli_model* m, const int32_t* prompt, int32_t n_prompt, int32_t max_length,
                       int32_t* tokens_out, float* logits_out);
+/* predict for batch sequences with their own prompts: prompts [batch][ld] (sequence b's first lens[b]
+ * ids), tokens_out [batch][max_length], logits_out optional [max_length][batch][local vocab]. */
+int sli_model_predict_batch(sli_model* m, const int32_t* prompts, const int32_t* lens, int32_t ld, int32_t max_length,
+                            int32_t* tokens_out, float* logits_out);
 /* Copy one layer's K (which=0) or V (which=1) cache, positions [0, upto), to host as fp32 in reference
  * layout [upto][KV_local]. */
 int sli_model_get_kv(sli_model* m, int32_t layer, int32_t which, int32_t upto, float* host);
+int sli_model_get_kv_seq(sli_model* m, int32_t seq, int32_t layer, int32_t which, int32_t upto, float* host);
 /* Read back this rank's shard of a weight (sli_tp_plan window, n = n_rows * n_cols) as fp32 (int8 is
  * dequantised with its row scales). */
 int sli_model_get_weight(sli_model* m, int32_t kind, int32_t index, float* host, int64_t n);

@@ -32,7 +32,7 @@ class ModelConfig(ctypes.Structure):
     _fields_ = [(n, c_i32) for n in ("vocab", "dim", "n_heads", "n_kv_heads", "head_dim", "ffn", "n_layers",
                                      "max_len")] + \
                [("eps", c_f), ("theta", c_f)] + \
-               [(n, c_i32) for n in ("w_dtype", "kv_dtype", "act_mode", "tp_rank", "tp_size", "device")]
+               [(n, c_i32) for n in ("w_dtype", "kv_dtype", "act_mode", "tp_rank", "tp_size", "device", "batch")]
 
 
 class ShardWindow(ctypes.Structure):
@@ -56,6 +56,8 @@ _SIGS = {
     "sli_stream_destroy": (c_int, [c_vp]),
     "sli_stream_sync": (c_int, [c_vp]),
     "sli_matmul": (c_int, [c_vp, c_vp, c_int, c_vp, c_vp, c_i32, c_i32, c_f, c_vp]),
+    "sli_matmul_batch_workspace_bytes": (c_sz, [c_i32, c_i32, c_i32]),
+    "sli_matmul_batch": (c_int, [c_vp, c_vp, c_int, c_vp, c_i32, c_i32, c_i32, c_vp, c_sz, c_vp]),
     "sli_rmsnorm": (c_int, [c_vp, c_vp, c_vp, c_i32, c_f, c_vp]),
     "sli_rope_cache": (c_int, [c_i32, c_i32, c_vp, c_vp, c_f, c_vp]),
     "sli_rope": (c_int, [c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp]),
@@ -80,11 +82,17 @@ _SIGS = {
     "sli_model_set_state": (c_int, [c_vp, c_i32, c_i32, c_i32]),
     "sli_model_set_prompt": (c_int, [c_vp, c_vp, c_i32]),
     "sli_model_get_state": (c_int, [c_vp, P_i32, P_i32, P_i32, P_i32]),
+    "sli_model_set_state_seq": (c_int, [c_vp, c_i32, c_i32, c_i32, c_i32]),
+    "sli_model_set_prompt_seq": (c_int, [c_vp, c_i32, c_vp, c_i32]),
+    "sli_model_get_state_seq": (c_int, [c_vp, c_i32, P_i32, P_i32, P_i32, P_i32]),
+    "sli_model_get_history": (c_int, [c_vp, c_i32, c_i32, c_vp]),
     "sli_model_step": (c_int, [c_vp]),
     "sli_model_sync": (c_int, [c_vp]),
     "sli_model_get_logits": (c_int, [c_vp, c_vp, c_i32, P_i32]),
     "sli_model_predict": (c_int, [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp]),
+    "sli_model_predict_batch": (c_int, [c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp]),
     "sli_model_get_kv": (c_int, [c_vp, c_i32, c_i32, c_i32, c_vp]),
+    "sli_model_get_kv_seq": (c_int, [c_vp, c_i32, c_i32, c_i32, c_i32, c_vp]),
     "sli_model_get_weight": (c_int, [c_vp, c_i32, c_i32, c_vp, c_i64]),
     "sli_model_stream": (c_int, [c_vp, ctypes.POINTER(c_vp)]),
     "sli_model_step_bytes": (c_int, [c_vp, P_d, P_d]),
@@ -122,6 +130,7 @@ def check(rc: int, where: str) -> None:
 
 def call(name: str, *args) -> int:
     rc = getattr(load(), name)(*args)
-    if isinstance(rc, int) and name not in ("sli_version", "sli_mha_workspace_bytes", "sli_comm_id_bytes"):
+    if isinstance(rc, int) and name not in ("sli_version", "sli_mha_workspace_bytes", "sli_comm_id_bytes",
+                                                 "sli_matmul_batch_workspace_bytes"):
         check(rc, name)
     return rc

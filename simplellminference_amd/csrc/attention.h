@@ -31,7 +31,15 @@ struct AttnArgs {
     int n_kv_heads;
     int max_splits;
     float scale;            // 1/sqrt(hd) (mha_kernel.cpp:41)
+    int seq_heads;          // kv heads per sequence: a batch is B sequences of seq_heads kv heads each
+    int pos_seq_stride;     // int32s between consecutive sequences' positions at pos_dev
 };
+
+// Position of the sequence that owns (batched) kv head kvh.
+template <typename KT>
+__device__ __forceinline__ int attn_pos(const AttnArgs<KT>& a, int kvh) {
+    return a.pos_dev ? a.pos_dev[(size_t)(kvh / a.seq_heads) * a.pos_seq_stride] : a.pos_host;
+}
 
 // A workgroup covers kAttnSlots wave-instructions of K (and of V) per lane-row group: WAVES waves of
 // NIT = kAttnSlots / WAVES vectors each. The split geometry (positions per workgroup) is therefore the
@@ -66,7 +74,7 @@ __device__ __forceinline__ bool attn_publish(const AttnArgs<KT>& a, int kvh, int
     __shared__ int last;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int pos = a.pos_dev ? *a.pos_dev : a.pos_host;
+    const int pos = attn_pos(a, kvh);
     if (wgs * WAVES * PPW > pos) return false;  // whole workgroup past the live context (uniform exit)
     const int t0 = (wgs * WAVES + wave) * PPW;
     const bool live_wave = t0 <= pos;
@@ -253,10 +261,9 @@ __device__ __forceinline__ void attn_merge(const float* part, float* out, int kv
 
 // Live split count of a kv head at position pos (workgroups that run attn_publish to the end).
 template <typename KT, int HD, int G>
-__device__ __forceinline__ int attn_live_splits(const AttnArgs<KT>& a) {
+__device__ __forceinline__ int attn_live_splits(const AttnArgs<KT>& a, int kvh) {
     constexpr int PPWG = AttnGeom<KT, HD>::PPWG;
-    const int pos = a.pos_dev ? *a.pos_dev : a.pos_host;
-    return min(pos / PPWG + 1, a.max_splits);
+    return min(attn_pos(a, kvh) / PPWG + 1, a.max_splits);
 }
 
 // grid: n_kv_heads * wg_splits workgroups of 64 * attn_waves(G) threads
@@ -264,7 +271,7 @@ template <typename KT, int HD, int G>
 __global__ void __launch_bounds__(64 * attn_waves(G)) attn_partial_kernel(AttnArgs<KT> a) {
     const int kvh = blockIdx.x / a.max_splits;  // max_splits counts workgroup splits here
     if (attn_publish<KT, HD, G>(a, kvh, blockIdx.x - kvh * a.max_splits))
-        attn_merge<HD, G>(a.part, a.out, kvh, a.max_splits, attn_live_splits<KT, HD, G>(a), 0, blockDim.x);
+        attn_merge<HD, G>(a.part, a.out, kvh, a.max_splits, attn_live_splits<KT, HD, G>(a, kvh), 0, blockDim.x);
 }
 
 }  // namespace sli

@@ -1,0 +1,485 @@
+// bgemm.h — batched decode projection on MFMA for gfx950: Y[b][row] = sum_k W[row][k] * X[b][k] for a
+// batch of B <= 8 sequences decoding in lockstep ("the N=8 skinny GEMM is the only
+// place MFMA pays"). It replaces the reference's one-row-per-block matmul_f32_kernel
+// (source/kernel/cuda/matmul_kernel.cu:5-38) for B > 1, with the same fused epilogues as the batch-1
+// GEMV (gemv.h): RMSNorm prologue (rms_kernel.cpp:5-23), RoPE + K/V cache write (rope_kernel.cpp:22-41),
+// SwiGLU (swiglu_kernel.cpp:5-15), residual add (add_kernel.cpp:5-14), logits + argmax keys.
+//
+// Shape of the work (fp16 weights, fp32 activations, fp32 accumulate):
+//   * the weight matrix is cut into 16-row tiles; the epilogue's tile row map lets a tile hold the RoPE
+//     partner rows {d, d + hd/2} or the {gate u, up u} rows together (tile rows i and i + 8);
+//   * v_mfma_f32_16x16x32_f16: A = 16 weight rows x 32 k straight from HBM (one 16-byte load per lane;
+//     cdna_hip_programming.md §3 fragment layout: lane l holds row l&15, k 8(l>>4)..+7), B = 16
+//     activation columns: column b < 8 is the fp16 high part of sequence b, column 8 + b its fp16 low
+//     part (x - fp16(x)); the fp32 input is carried to ~2^-22 at no MFMA cost (the 8 spare columns of a
+//     batch-8 tile) and hi + lo are summed in fp32 after the MFMA;
+//   * a workgroup owns `tpw` consecutive tiles and one of `splits` contiguous k-ranges; its 16 waves split
+//     the k-range of the current tile, stream it with the next two steps' loads in flight, and their 16
+//     partials are reduced in LDS by one wave per tile (round-robin, off the other waves' path);
+//   * the activations of the k-range are staged once per workgroup in LDS in the B-fragment layout
+//     (lane-linear 16-byte slots: conflict-free ds_read_b128), RMS-normalised per sequence when fused;
+//   * splits > 1: per-tile partials are published write-through (sc1) and the group's last-arriving
+//     workgroup sums them in split order (deterministic) and runs the epilogue (the hand-off recipe of
+//     attention.h, MI355X_MICROARCH.md).
+#pragma once
+#include "common.h"
+
+namespace sli {
+
+typedef _Float16 bg_half8 __attribute__((ext_vector_type(8)));
+typedef float bg_float4 __attribute__((ext_vector_type(4)));
+
+constexpr int kBgThreads = 1024;
+constexpr int kBgWaves = kBgThreads / 64;
+constexpr int kBgMaxBatch = 8;
+constexpr int kBgNH = 4;               // staged half-slots (8 k of one sequence) per thread
+constexpr int kBgMaxStageElems = kBgNH * kBgThreads * 8;  // B * (staged k) <= 32768
+constexpr int kBgScratch = 1024;       // bytes: ss partials [16][8] f32, inv [8] f32, keys [8] u64, flag
+constexpr int kBgKeysOff = 640;
+constexpr int kBgFlagOff = 704;
+constexpr int kBgPBytes = 2 * kBgWaves * 16 * 8 * 4;  // double-buffered per-wave tile partials
+constexpr int kBgLdsMax = 160 * 1024;
+constexpr int kBgU = 4;                // 16-byte weight loads per lane per step (two steps in flight)
+
+struct BgIn {
+    const float* x;       // [B][K] fp32 activations
+    const float* norm_w;  // fused RMSNorm weight [K], or nullptr
+    float eps;
+    int K;
+    int B;
+    int ntiles;           // 16-row output tiles
+    int tpw;              // tiles per workgroup
+    int splits;           // k-ranges (workgroups per tile group)
+    float* ws;            // splits > 1: partials [ntiles][splits][16][8]
+    unsigned* counters;   // splits > 1: [groups] arrival counters, zero between launches
+};
+
+// ---------------------------------------------------------------- host-side plan
+struct BgPlan {
+    int ntiles = 0, tpw = 1, splits = 1, groups = 0;
+    size_t lds = 0;
+};
+
+inline size_t bg_lds_bytes(int K, int splits, int tpw) {
+    const int nkb = K / 32;
+    const int kbs = (nkb + splits - 1) / splits;
+    return (size_t)kBgScratch + (size_t)kbs * 1024 + kBgPBytes + (size_t)tpw * 512;
+}
+
+// (tiles per workgroup, k-splits) for a [16*ntiles x K] weight: about one workgroup per CU, the activation
+// staging amortised over several tiles (B*K/splits*4 bytes from L2 per workgroup, plus B*K*4 for the
+// fused RMS over the full row), the LDS image within 160 KiB. Cost in units of one 16x32 fp16 weight
+// block (1 KiB of HBM); L2 bytes priced at a quarter of HBM bytes.
+inline BgPlan bg_plan(int ntiles, int K, int B, bool norm, int cus = 256) {
+    const int nkb = K / 32;
+    BgPlan best;
+    double best_cost = 1e30;
+    for (int s = 1; s <= 16; ++s) {
+        if (s > 1 && nkb / s < kBgWaves) break;  // every wave keeps at least one block per tile
+        const int kbs = (nkb + s - 1) / s;
+        if ((size_t)B * kbs * 32 > (size_t)kBgMaxStageElems) continue;  // staging registers
+        for (int tpw = 1; tpw <= 64; ++tpw) {
+            if (bg_lds_bytes(K, s, tpw) > (size_t)kBgLdsMax) break;
+            const int groups = (ntiles + tpw - 1) / tpw;
+            const int wgs = groups * s;
+            const int rounds = (wgs + cus - 1) / cus;
+            double per_wg = (double)tpw * kbs + 0.25 * kbs * B / 8.0 + 40.0;
+            if (norm) per_wg += 0.25 * nkb * B / 8.0;
+            if (s > 1) per_wg += 20.0 + 0.5 * s * tpw;
+            const double cost = rounds * per_wg;
+            if (cost < best_cost - 1e-9) {
+                best_cost = cost;
+                best.ntiles = ntiles;
+                best.tpw = tpw;
+                best.splits = s;
+                best.groups = groups;
+                best.lds = bg_lds_bytes(K, s, tpw);
+            }
+            if (groups == 1) break;
+        }
+    }
+    return best;
+}
+
+// device workspace of a plan: split partials (256-B aligned), then one arrival counter per group
+inline size_t bg_part_bytes(const BgPlan& p) {
+    return p.splits > 1 ? (((size_t)p.ntiles * p.splits * 128 * sizeof(float) + 255) & ~(size_t)255) : 0;
+}
+inline size_t bg_ws_bytes(const BgPlan& p) { return bg_part_bytes(p) + sizeof(unsigned) * (size_t)p.groups + 256; }
+
+// ---------------------------------------------------------------- device side
+__device__ __forceinline__ bg_float4 bg_mfma(const u32x4& a, const u32x4& b, bg_float4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(bg_half8, a), __builtin_bit_cast(bg_half8, b), c,
+                                                  0, 0, 0);
+}
+
+__device__ __forceinline__ float bg_load_sc1(const float* base, unsigned bytes, unsigned off) {
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, bytes, 0x00020000);
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 16 /* sc1 */));
+}
+
+// fp32 -> (fp16 hi, fp16 lo), hi + lo == v to ~2^-22 relative
+__device__ __forceinline__ void bg_split8(const float* y, u32x4& hi, u32x4& lo) {
+    unsigned h[4], l[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const _Float16 h0 = (_Float16)y[2 * p], h1 = (_Float16)y[2 * p + 1];
+        const _Float16 l0 = (_Float16)(y[2 * p] - (float)h0), l1 = (_Float16)(y[2 * p + 1] - (float)h1);
+        h[p] = (unsigned)__builtin_bit_cast(unsigned short, h0) | ((unsigned)__builtin_bit_cast(unsigned short, h1) << 16);
+        l[p] = (unsigned)__builtin_bit_cast(unsigned short, l0) | ((unsigned)__builtin_bit_cast(unsigned short, l1) << 16);
+    }
+    hi = u32x4{h[0], h[1], h[2], h[3]};
+    lo = u32x4{l[0], l[1], l[2], l[3]};
+}
+
+// Epilogue contract (a mutable copy per thread):
+//   row(t, i)                   weight row of tile t's row i (i < 16), always a valid row (clamped)
+//   store(t, i, b, v0, v1, kl)  final sums of tile rows i (< 8) and i + 8 for sequence b; kl = the
+//                               workgroup's per-sequence argmax keys in LDS
+//   finish(kl, group, B)        once per workgroup that ran stores, after all of them
+template <class Epi, bool NORM>
+__global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restrict__ W, BgIn in, Epi epi_in) {
+    Epi epi = epi_in;
+    extern __shared__ __attribute__((aligned(16))) char bg_smem[];
+    float* red = reinterpret_cast<float*>(bg_smem);  // [16][8]
+    float* inv = red + kBgWaves * 8;                 // [8]
+    unsigned long long* keys = reinterpret_cast<unsigned long long*>(bg_smem + kBgKeysOff);
+    int* flag = reinterpret_cast<int*>(bg_smem + kBgFlagOff);
+    u32x4* img = reinterpret_cast<u32x4*>(bg_smem + kBgScratch);
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int S = in.splits, K = in.K, B = in.B;
+    const int g = blockIdx.x / S, s = blockIdx.x - g * S;
+    const int nkb = K >> 5;
+    const int kb0 = (s * nkb) / S, nkbs = ((s + 1) * nkb) / S - kb0;  // this split's 32-k blocks
+    const int kbs_max = (nkb + S - 1) / S;
+    float* P = reinterpret_cast<float*>(bg_smem + kBgScratch + (size_t)kbs_max * 1024);  // [2][16 waves][16][8]
+    float* R = P + 2 * kBgWaves * 128;                                                 // [tpw][16][8]
+    const int t0 = g * in.tpw;
+    const int ntg = min(in.tpw, in.ntiles - t0);  // this workgroup's tiles (uniform)
+    const int wb0 = kb0 + (wave * nkbs) / kBgWaves;  // this wave's blocks of every tile
+    const int wnb = kb0 + ((wave + 1) * nkbs) / kBgWaves - wb0;
+    const int per_wave_max = (nkbs + kBgWaves - 1) / kBgWaves;
+    const int cpt = max((per_wave_max + kBgU - 1) / kBgU, 1);  // steps per tile (uniform)
+    const int nsteps = ntg * cpt;
+
+    if (tid < kBgMaxBatch) keys[tid] = 0ull;
+
+    // ---- 1. activation staging loads, issued first (s_waitcnt vmcnt counts in issue order)
+    const int n8 = NORM ? (K >> 3) : (nkbs << 2);  // half-slots per sequence in the staged range
+    const int k8_0 = NORM ? 0 : (kb0 << 2);
+    const int nhs = B * n8;
+    float4 xa[kBgNH][2], xw[kBgNH][2];
+#pragma unroll
+    for (int n = 0; n < kBgNH; ++n) {
+        const int h = min(tid + n * kBgThreads, nhs - 1);  // clamp, never branch around a load
+        const int b = h / n8, k8 = k8_0 + (h - b * n8);
+        const float4* xp = reinterpret_cast<const float4*>(in.x + (size_t)b * K + (size_t)k8 * 8);
+        xa[n][0] = xp[0];
+        xa[n][1] = xp[1];
+        if constexpr (NORM) {
+            const float4* wp = reinterpret_cast<const float4*>(in.norm_w + (size_t)k8 * 8);
+            xw[n][0] = wp[0];
+            xw[n][1] = wp[1];
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+
+    // ---- 2. the first two weight steps
+    const size_t row_bytes = (size_t)K * 2;
+    const int q8 = (lane >> 4) * 8;  // this lane's k offset inside a 32-k block
+    auto load_step = [&](int k, u32x4(&w)[kBgU]) {
+        const int kk = min(k, nsteps - 1);
+        const int j = kk / cpt, c = kk - j * cpt;
+        const int row = epi.row(t0 + j, lane & 15);
+        const char* base = reinterpret_cast<const char*>(W) + (size_t)row * row_bytes + (size_t)q8 * 2;
+#pragma unroll
+        for (int u = 0; u < kBgU; ++u) {
+            const int bi = wb0 + min(c * kBgU + u, max(wnb - 1, 0));
+            w[u] = load16<true>(base + (size_t)bi * 64);
+        }
+    };
+    u32x4 wa[kBgU], wb[kBgU];
+    load_step(0, wa);
+    load_step(1, wb);
+    __builtin_amdgcn_sched_barrier(0);
+
+    // ---- 3. per-sequence RMS over the full K (rms_kernel.cpp:12-19)
+    if constexpr (NORM) {
+        float ssb[kBgMaxBatch];
+#pragma unroll
+        for (int b = 0; b < kBgMaxBatch; ++b) ssb[b] = 0.0f;
+#pragma unroll
+        for (int n = 0; n < kBgNH; ++n) {
+            const int h = tid + n * kBgThreads;
+            const int b = min(h, nhs - 1) / n8;
+            float v = 0.0f;
+            v += xa[n][0].x * xa[n][0].x;
+            v += xa[n][0].y * xa[n][0].y;
+            v += xa[n][0].z * xa[n][0].z;
+            v += xa[n][0].w * xa[n][0].w;
+            v += xa[n][1].x * xa[n][1].x;
+            v += xa[n][1].y * xa[n][1].y;
+            v += xa[n][1].z * xa[n][1].z;
+            v += xa[n][1].w * xa[n][1].w;
+            v = h < nhs ? v : 0.0f;
+#pragma unroll
+            for (int bb = 0; bb < kBgMaxBatch; ++bb) ssb[bb] += bb == b ? v : 0.0f;
+        }
+#pragma unroll
+        for (int bb = 0; bb < kBgMaxBatch; ++bb) {
+            const float t = wave_sum(ssb[bb]);
+            if (lane == 0) red[wave * 8 + bb] = t;
+        }
+        __syncthreads();
+        if (tid < B) {
+            float t = 0.0f;
+            for (int w = 0; w < kBgWaves; ++w) t += red[w * 8 + tid];
+            const float tep = t / (float)K;         // rms_kernel.cpp:17
+            const float rms = sqrtf(tep + in.eps);  // :18
+            inv[tid] = 1.0f / rms;                  // :19
+        }
+        __syncthreads();
+    }
+
+    // ---- 4. the split's k-range of every sequence into LDS as B fragments (hi: column b, lo: 8 + b)
+#pragma unroll
+    for (int n = 0; n < kBgNH; ++n) {
+        const int h = tid + n * kBgThreads;
+        const int hc = min(h, nhs - 1);
+        const int b = hc / n8, k8 = k8_0 + (hc - b * n8);
+        const int rel = k8 - (kb0 << 2);  // half-slot inside the split's range
+        if (h < nhs && rel >= 0 && rel < (nkbs << 2)) {
+            float y[8] = {xa[n][0].x, xa[n][0].y, xa[n][0].z, xa[n][0].w,
+                          xa[n][1].x, xa[n][1].y, xa[n][1].z, xa[n][1].w};
+            if constexpr (NORM) {
+                const float iv = inv[b];
+                const float wv[8] = {xw[n][0].x, xw[n][0].y, xw[n][0].z, xw[n][0].w,
+                                     xw[n][1].x, xw[n][1].y, xw[n][1].z, xw[n][1].w};
+#pragma unroll
+                for (int e = 0; e < 8; ++e) y[e] = (y[e] * iv) * wv[e];  // rms_kernel.cpp:20-22
+            }
+            u32x4 hi, lo;
+            bg_split8(y, hi, lo);
+            const int ib = rel >> 2, q = rel & 3;
+            img[ib * 64 + q * 16 + b] = hi;
+            img[ib * 64 + q * 16 + 8 + b] = lo;
+        }
+    }
+    __syncthreads();
+
+    // ---- 5. stream the tiles
+    bg_float4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    const u32x4* wimg = img + (size_t)(wb0 - kb0) * 64 + lane;
+    auto consume = [&](int k, const u32x4(&w)[kBgU]) {
+        const int j = k / cpt, c = k - j * cpt;
+#pragma unroll
+        for (int u = 0; u < kBgU; ++u) {
+            const int r = c * kBgU + u;
+            if (r < wnb) acc = bg_mfma(w[u], wimg[(size_t)r * 64], acc);
+        }
+        if (c == cpt - 1) {  // tile j complete in every wave (uniform branch)
+            float* Pb = P + (j & 1) * (kBgWaves * 128);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[r] += __shfl_xor(acc[r], 8, kWave);  // hi + lo columns
+            if ((lane & 8) == 0) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) Pb[wave * 128 + ((lane >> 4) * 4 + r) * 8 + (lane & 7)] = acc[r];
+            }
+            acc = bg_float4{0.0f, 0.0f, 0.0f, 0.0f};
+            __syncthreads();
+            if (wave == (j & (kBgWaves - 1))) {  // tile j's 16 wave partials, summed in wave order
+                const int i = lane >> 3, b = lane & 7;
+                float v0 = 0.0f, v1 = 0.0f;
+#pragma unroll
+                for (int w = 0; w < kBgWaves; ++w) {
+                    v0 += Pb[w * 128 + i * 8 + b];
+                    v1 += Pb[w * 128 + (i + 8) * 8 + b];
+                }
+                R[j * 128 + i * 8 + b] = v0;
+                R[j * 128 + (i + 8) * 8 + b] = v1;
+            }
+        }
+    };
+    int k = 0;
+    for (; k + 2 < nsteps; k += 2) {
+        consume(k, wa);
+        load_step(k + 2, wa);
+        consume(k + 1, wb);
+        load_step(k + 3, wb);
+    }
+    if (k < nsteps) consume(k, wa);
+    if (k + 1 < nsteps) consume(k + 1, wb);
+    __syncthreads();
+
+    // ---- 6. epilogue (one split) or publish + the group's last arriver merges in split order
+    const int items = ntg * 64;  // (tile, row pair i < 8, sequence slot b < 8)
+    if (S == 1) {
+        for (int it = tid; it < items; it += kBgThreads) {
+            const int j = it >> 6, i = (it >> 3) & 7, b = it & 7;
+            if (b < B) epi.store(t0 + j, i, b, R[j * 128 + i * 8 + b], R[j * 128 + (i + 8) * 8 + b], keys);
+        }
+    } else {
+        for (int e = tid; e < ntg * 128; e += kBgThreads) {
+            const int j = e >> 7, r = e & 127;
+            __hip_atomic_store(in.ws + ((size_t)(t0 + j) * S + s) * 128 + r, R[e], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before the arrival
+        __syncthreads();
+        if (tid == 0) {
+            const unsigned prev = __hip_atomic_fetch_add(in.counters + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            *flag = prev == (unsigned)(S - 1);
+            if (*flag) __hip_atomic_store(in.counters + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        if (*flag == 0) return;  // uniform
+        const float* base = in.ws + (size_t)t0 * S * 128;
+        const unsigned bytes = (unsigned)(sizeof(float) * (size_t)ntg * S * 128);
+        for (int it = tid; it < items; it += kBgThreads) {
+            const int j = it >> 6, i = (it >> 3) & 7, b = it & 7;
+            if (b >= B) continue;
+            float v0 = 0.0f, v1 = 0.0f;
+            for (int sp = 0; sp < S; ++sp) {  // split order: deterministic
+                const unsigned o = (unsigned)((j * S + sp) * 128);
+                v0 += bg_load_sc1(base, bytes, 4u * (o + i * 8 + b));
+                v1 += bg_load_sc1(base, bytes, 4u * (o + (i + 8) * 8 + b));
+            }
+            epi.store(t0 + j, i, b, v0, v1, keys);
+        }
+    }
+    epi.finish(keys, g, B);
+}
+
+// ---------------------------------------------------------------- epilogues
+// Plain rows: tile t holds rows 16t .. 16t+15. y[b][row] = resid[b][row] + (sum * rscale[row]) * scale
+// (matmul_kernel.cpp:26 fused with add_kernel.cpp:5-14).
+struct BgEpiStore {
+    float* y;
+    const float* resid;
+    const float* rscale;
+    float scale;
+    int nrows;
+    int ld;  // per-sequence stride of y / resid
+    __device__ int row(int t, int i) const { return min(t * 16 + i, nrows - 1); }
+    __device__ void one(int row, int b, float v) const {
+        if (row >= nrows) return;
+        float a = rscale ? v * rscale[row] : v;
+        a = a * scale;
+        const size_t o = (size_t)b * ld + row;
+        y[o] = resid ? resid[o] + a : a;
+    }
+    __device__ void store(int t, int i, int b, float v0, float v1, unsigned long long*) const {
+        one(t * 16 + i, b, v0);
+        one(t * 16 + i + 8, b, v1);
+    }
+    __device__ void finish(unsigned long long*, int, int) const {}
+};
+
+// Fused q/k/v + RoPE + K/V cache write (model.cpp:54-67) per sequence: tile rows i and i + 8 are the
+// RoPE pair {d, d + hd/2} of one head (8 pairs per tile). Cache [B][hkv][T][hd] per layer; sequence b's
+// position is pos_dev[b * pos_stride].
+template <typename KT>
+struct BgEpiQKV {
+    float* q_out;  // [B][hq*hd]
+    KT* kc;        // layer base
+    KT* vc;
+    const int32_t* pos_dev;
+    int pos_stride;
+    const float* sin_t;
+    const float* cos_t;
+    int hq, hkv, hd, T;
+    __device__ int row(int t, int i) const {
+        const int half = hd >> 1;
+        const int u = t * 8 + (i & 7);
+        const int uh = u / half, d = u - uh * half;
+        return uh * hd + d + (i >= 8 ? half : 0);
+    }
+    __device__ void store(int t, int i, int b, float a0, float a1, unsigned long long*) const {
+        const int half = hd >> 1;
+        const int u = t * 8 + i;
+        const int uh = u / half, d = u - uh * half;
+        const int pos = pos_dev[(size_t)b * pos_stride];
+        if (uh < hq + hkv) {  // rope_kernel.cpp:30-38
+            const float fci = sin_t[pos * half + d], fcr = cos_t[pos * half + d];
+            const float r0 = a0 * fcr - a1 * fci;
+            const float r1 = a1 * fcr + a0 * fci;
+            if (uh < hq) {
+                float* q = q_out + ((size_t)b * hq + uh) * hd;
+                q[d] = r0;
+                q[d + half] = r1;
+            } else {
+                KT* kp = kc + (((size_t)b * hkv + (uh - hq)) * T + pos) * hd;
+                kp[d] = from_f32<KT>(r0);
+                kp[d + half] = from_f32<KT>(r1);
+            }
+        } else {
+            KT* vp = vc + (((size_t)b * hkv + (uh - hq - hkv)) * T + pos) * hd;
+            vp[d] = from_f32<KT>(a0);
+            vp[d + half] = from_f32<KT>(a1);
+        }
+    }
+    __device__ void finish(unsigned long long*, int, int) const {}
+};
+
+// Fused gate/up + activation (model.cpp:99-115): fused rows [gate(I); up(I)]; tile rows i / i + 8 are
+// gate u / up u for u = 8t + i.
+struct BgEpiSwiGLU {
+    float* act;  // [B][inter]
+    int inter;
+    int silu;
+    __device__ int row(int t, int i) const { return t * 8 + (i & 7) + (i >= 8 ? inter : 0); }
+    __device__ void store(int t, int i, int b, float g, float up, unsigned long long*) const {
+        float sg = 1.0f / (1.0f + expf(-g));  // swiglu_kernel.cpp:12
+        if (silu) sg = g * sg;
+        act[(size_t)b * inter + t * 8 + i] = sg * up;  // :13
+    }
+    __device__ void finish(unsigned long long*, int, int) const {}
+};
+
+// LM head (model.cpp:136-139) per sequence + the first stage of the device argmax: the workgroup that
+// ran a group's stores writes each sequence's max orderable key to keys_out[b][group].
+struct BgEpiLogits {
+    float* logits;                 // [B][ld]
+    unsigned long long* keys_out;  // [B][key_ld]
+    int nrows, ld, vocab_off, key_ld;
+    __device__ int row(int t, int i) const { return min(t * 16 + i, nrows - 1); }
+    __device__ void one(int row, int b, float v, unsigned long long* kl) const {
+        if (row >= nrows) return;
+        logits[(size_t)b * ld + row] = v;
+        atomicMax(kl + b, argmax_key(v, (unsigned)(row + vocab_off)));  // a max: order-independent
+    }
+    __device__ void store(int t, int i, int b, float v0, float v1, unsigned long long* kl) const {
+        one(t * 16 + i, b, v0, kl);
+        one(t * 16 + i + 8, b, v1, kl);
+    }
+    __device__ void finish(unsigned long long* kl, int g, int B) const {
+        __syncthreads();
+        if ((int)threadIdx.x < B) keys_out[(size_t)threadIdx.x * key_ld + g] = kl[threadIdx.x];
+    }
+};
+
+// Allow the kernel its full dynamic LDS (once per instantiation; call outside stream capture).
+template <class Epi, bool NORM>
+hipError_t bg_allow_lds() {
+    static const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&bgemm_kernel<Epi, NORM>),
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize, kBgLdsMax);
+    return e;
+}
+
+template <class Epi>
+hipError_t launch_bgemm(const __half* W, const BgIn& in_, const Epi& epi, const BgPlan& p, hipStream_t s) {
+    BgIn in = in_;
+    in.ntiles = p.ntiles;
+    in.tpw = p.tpw;
+    in.splits = p.splits;
+    const dim3 grid(p.groups * p.splits);
+    if (in.norm_w)
+        hipLaunchKernelGGL((bgemm_kernel<Epi, true>), grid, dim3(kBgThreads), p.lds, s, W, in, epi);
+    else
+        hipLaunchKernelGGL((bgemm_kernel<Epi, false>), grid, dim3(kBgThreads), p.lds, s, W, in, epi);
+    return hipGetLastError();
+}
+
+}  // namespace sli

@@ -25,6 +25,7 @@
 
 #include "../../include/sli_synth.h"
 #include "attention.h"
+#include "bgemm.h"
 #include "common.h"
 #include "gemv.h"
 #include "ops_internal.h"
@@ -74,6 +75,13 @@ struct sli_model {
     hipGraph_t graph = nullptr;
     hipGraphExec_t graph_exec = nullptr;
     std::vector<void*> allocs;
+    // batch > 1: B sequences decode in lockstep, the projections run on MFMA (bgemm.h)
+    int B = 1;
+    sli::BgPlan bp_qkv, bp_wo, bp_gu, bp_down, bp_lm;
+    float* bg_ws = nullptr;               // split-K partials of the batched projections
+    unsigned* bg_cnt = nullptr;           // their arrival counters (zero between launches)
+    unsigned long long* bkeys = nullptr;  // [B] per-sequence argmax keys (all-reduced MAX under TP)
+    int key_ld = sli::kGemvMaxBlocks;     // per-sequence stride of the per-workgroup argmax keys
 };
 
 namespace sli {
@@ -241,21 +249,61 @@ __global__ void finalize_kernel(DevState* st, const int32_t* __restrict__ prompt
     finalize_state(st, prompt, hist, T);
 }
 
+// ---- batch > 1: one sequence per block / thread
+// emb_kernel.cpp:4-21 per sequence, token read on device (graph-capturable)
+template <typename T>
+__global__ void embedding_batch_kernel(const DevState* st, const T* __restrict__ table, const float* row_scale,
+                                       float* __restrict__ out, int vocab, int dim) {
+    const int b = blockIdx.y;
+    const int token = st[b].token;
+    const bool ok = token >= 0 && token < vocab;
+    const float s = (ok && row_scale) ? row_scale[token] : 1.0f;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < dim; i += gridDim.x * blockDim.x)
+        out[(size_t)b * dim + i] = ok ? to_f32(table[(size_t)token * dim + i]) * s : 0.0f;
+}
+
+// second argmax stage per sequence: block b reduces keys[b][0 .. n) into out[b]
+__global__ void keyreduce_batch_kernel(const unsigned long long* __restrict__ keys, int ld, int n,
+                                       unsigned long long* out) {
+    const unsigned long long* k = keys + (size_t)blockIdx.x * ld;
+    unsigned long long b = 0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) b = k[i] > b ? k[i] : b;
+    b = wave_max_u64(b);
+    __shared__ unsigned long long red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = b;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) b = red[w] > b ? red[w] : b;
+        out[blockIdx.x] = b;
+    }
+}
+
+__global__ void finalize_batch_kernel(DevState* st, const unsigned long long* __restrict__ keys,
+                                      const int32_t* __restrict__ prompt, int32_t* hist, int T, int B) {
+    const int b = threadIdx.x;
+    if (b >= B) return;
+    st[b].key = keys[b];
+    finalize_state(st + b, prompt + (size_t)b * (T + 1), hist + (size_t)b * (T + 1), T);
+}
+
 template <typename KT>
-__global__ void fill_kv_kernel(KT* kc, KT* vc, int L, int hkv, int T, int hd, int upto, int kv_full, int head_lo,
-                               uint32_t seed, float c) {
-    const uint64_t n = (uint64_t)L * hkv * upto * hd;
+__global__ void fill_kv_kernel(KT* kc, KT* vc, int L, int B, int hkv, int T, int hd, int upto, int kv_full,
+                               int head_lo, uint32_t seed, float c) {
+    const uint64_t n = (uint64_t)L * B * hkv * upto * hd;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const int d = (int)(i % hd);
         uint64_t rest = i / hd;
         const int t = (int)(rest % upto);
         rest /= upto;
         const int h = (int)(rest % hkv);
-        const int l = (int)(rest / hkv);
+        rest /= hkv;
+        const int b = (int)(rest % B);
+        const int l = (int)(rest / B);
         const uint64_t idx = (uint64_t)t * kv_full + (uint64_t)(head_lo + h) * hd + d;  // reference layout index
-        const size_t off = (((size_t)l * hkv + h) * T + t) * hd + d;
-        kc[off] = from_f32<KT>(__fmul_rn((float)sli_rng_ih4(seed, sli_stream_id(SLI_T_KCACHE, l), idx), c));
-        vc[off] = from_f32<KT>(__fmul_rn((float)sli_rng_ih4(seed, sli_stream_id(SLI_T_VCACHE, l), idx), c));
+        const size_t off = ((((size_t)l * B + b) * hkv + h) * T + t) * hd + d;
+        const uint32_t sb = seed + (uint32_t)b;  // sequence b = the oracle's fill with seed + b
+        kc[off] = from_f32<KT>(__fmul_rn((float)sli_rng_ih4(sb, sli_stream_id(SLI_T_KCACHE, l), idx), c));
+        vc[off] = from_f32<KT>(__fmul_rn((float)sli_rng_ih4(sb, sli_stream_id(SLI_T_VCACHE, l), idx), c));
     }
 }
 
@@ -313,13 +361,106 @@ struct StepRecorder {
         return SLI_OK;
     }
     static int allreduce_x(sli_model* m) {
+        const size_t n = (size_t)m->B * m->D;
         if (m->collectives)
-            SLI_NCCL(ncclAllReduce(m->xpart, m->x, m->D, ncclFloat32, ncclSum, m->comm, m->stream));
+            SLI_NCCL(ncclAllReduce(m->xpart, m->x, n, ncclFloat32, ncclSum, m->comm, m->stream));
         else if (m->partial)  // debug no-comm mode: keep the local partial as the residual stream
-            SLI_HIP(hipMemcpyAsync(m->x, m->xpart, sizeof(float) * m->D, hipMemcpyDeviceToDevice, m->stream));
+            SLI_HIP(hipMemcpyAsync(m->x, m->xpart, sizeof(float) * n, hipMemcpyDeviceToDevice, m->stream));
         return SLI_OK;
     }
+
+    // ---- batch > 1: the same step for B sequences, projections on MFMA (bgemm.h)
+    static constexpr int kPosStride = (int)(sizeof(DevState) / sizeof(int32_t));
+    template <class Epi>
+    static int bg(sli_model* m, const void* W, const BgIn& in, const Epi& e, const BgPlan& p) {
+        if constexpr (std::is_same<WT, __half>::value) {
+            SLI_HIP(launch_bgemm((const __half*)W, in, e, p, m->stream));
+            return SLI_OK;
+        } else {
+            return fail(SLI_ERR_ARG, "batch > 1 needs fp16 weights");
+        }
+    }
+    template <class Epi, bool NORM>
+    static int allow(sli_model*) {
+        if constexpr (std::is_same<WT, __half>::value) SLI_HIP((bg_allow_lds<Epi, NORM>()));
+        return SLI_OK;
+    }
+    // raise the LDS limit of every batched kernel once, before any capture
+    static int prepare(sli_model* m) {
+        SLI_TRY((allow<BgEpiQKV<KT>, true>(m)));
+        SLI_TRY((allow<BgEpiStore, false>(m)));
+        SLI_TRY((allow<BgEpiSwiGLU, true>(m)));
+        SLI_TRY((allow<BgEpiLogits, true>(m)));
+        return SLI_OK;
+    }
+    static BgIn bin(sli_model* m, const float* x, const float* norm, int K) {
+        BgIn in{};
+        in.x = x;
+        in.norm_w = norm;
+        in.eps = m->c.eps;
+        in.K = K;
+        in.B = m->B;
+        in.ws = m->bg_ws;
+        in.counters = m->bg_cnt;
+        return in;
+    }
+    static int b_qkv(sli_model* m, int l) {
+        const size_t lay = (size_t)l * m->B * m->hkv * m->T * m->hd;
+        BgEpiQKV<KT> e{m->q, (KT*)m->kc + lay, (KT*)m->vc + lay, &m->st->pos, kPosStride, m->sin_t, m->cos_t,
+                       m->hq, m->hkv, m->hd, m->T};
+        return bg(m, m->layers[l].qkv, bin(m, m->x, m->norms + (size_t)(2 * l) * m->D, m->D), e, m->bp_qkv);
+    }
+    static int b_wo(sli_model* m, int l) {
+        const bool tp = m->partial;
+        BgEpiStore e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, nullptr, 1.0f, m->D, m->D};
+        return bg(m, m->layers[l].wo, bin(m, m->attn, nullptr, m->hq * m->hd), e, m->bp_wo);
+    }
+    static int b_gu(sli_model* m, int l) {
+        BgEpiSwiGLU e{m->act, m->Il, m->c.act_mode};
+        return bg(m, m->layers[l].gu, bin(m, m->x, m->norms + (size_t)(2 * l + 1) * m->D, m->D), e, m->bp_gu);
+    }
+    static int b_down(sli_model* m, int l) {
+        const bool tp = m->partial;
+        BgEpiStore e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, nullptr, 1.0f, m->D, m->D};
+        return bg(m, m->layers[l].down, bin(m, m->act, nullptr, m->Il), e, m->bp_down);
+    }
+    static int b_lm(sli_model* m) {
+        BgEpiLogits e{m->logits, m->keys, m->v_n, m->v_n, m->v_lo, m->key_ld};
+        const void* w = wptr(m->emb, m->wbytes, (size_t)m->v_lo * m->D);
+        return bg(m, w, bin(m, m->x, m->norms + (size_t)(2 * m->L) * m->D, m->D), e, m->bp_lm);
+    }
+    static int record_batched(sli_model* m) {
+        hipStream_t s = m->stream;
+        const int eb = std::min(64, (m->D + 255) / 256);
+        hipLaunchKernelGGL(embedding_batch_kernel<WT>, dim3(eb, m->B), dim3(256), 0, s, m->st, (const WT*)m->emb,
+                           m->emb_s, m->x, m->V, m->D);
+        SLI_HIP(hipGetLastError());
+        const long long ps = m->hd, hs = (long long)m->T * m->hd, ls = (long long)m->B * m->hkv * m->T * m->hd;
+        for (int l = 0; l < m->L; ++l) {
+            SLI_TRY(b_qkv(m, l));
+            // the batch is B * hkv kv heads of one layer: sequence b owns kv heads [b*hkv, (b+1)*hkv)
+            SLI_TRY(mha_launch<KT>(m->q, (const KT*)m->kc, (const KT*)m->vc, m->attn, l, 0, &m->st->pos, m->T, m->hd,
+                                   m->B * m->hq, m->B * m->hkv, ps, hs, ls, m->part, m->attn_count, s, m->hkv,
+                                   kPosStride));
+            SLI_TRY(b_wo(m, l));
+            SLI_TRY(allreduce_x(m));
+            SLI_TRY(b_gu(m, l));
+            SLI_TRY(b_down(m, l));
+            SLI_TRY(allreduce_x(m));
+        }
+        SLI_TRY(b_lm(m));
+        hipLaunchKernelGGL(keyreduce_batch_kernel, dim3(m->B), dim3(256), 0, s, m->keys, m->key_ld, m->bp_lm.groups,
+                           m->bkeys);
+        SLI_HIP(hipGetLastError());
+        if (m->collectives) SLI_NCCL(ncclAllReduce(m->bkeys, m->bkeys, m->B, ncclUint64, ncclMax, m->comm, s));
+        hipLaunchKernelGGL(finalize_batch_kernel, dim3(1), dim3(64), 0, s, m->st, m->bkeys, m->prompt, m->hist, m->T,
+                           m->B);
+        SLI_HIP(hipGetLastError());
+        return SLI_OK;
+    }
+
     static int record(sli_model* m) {
+        if (m->B > 1) return record_batched(m);
         hipStream_t s = m->stream;
         SLI_TRY(embedding_launch(0, &m->st->token, m->emb, m->c.w_dtype, m->emb_s, m->x, m->V, m->D, s));
         const long long ps = m->hd, hs = (long long)m->T * m->hd, ls = (long long)m->hkv * m->T * m->hd;
@@ -343,6 +484,15 @@ struct StepRecorder {
     }
     // All weight-streaming launches of one step (for the roofline probe).
     static int gemvs(sli_model* m) {
+        if (m->B > 1) {
+            for (int l = 0; l < m->L; ++l) {
+                SLI_TRY(b_qkv(m, l));
+                SLI_TRY(b_wo(m, l));
+                SLI_TRY(b_gu(m, l));
+                SLI_TRY(b_down(m, l));
+            }
+            return b_lm(m);
+        }
         for (int l = 0; l < m->L; ++l) {
             SLI_TRY(gemv_qkv(m, l));
             SLI_TRY(gemv_wo(m, l));
@@ -352,16 +502,16 @@ struct StepRecorder {
         return gemv_lm(m);
     }
     static int fill_kv(sli_model* m, uint32_t seed, int upto) {
-        const uint64_t n = (uint64_t)m->L * m->hkv * upto * m->hd;
+        const uint64_t n = (uint64_t)m->L * m->B * m->hkv * upto * m->hd;
         const int blocks = (int)std::min<uint64_t>(4096, (n + 255) / 256);
         hipLaunchKernelGGL(fill_kv_kernel<KT>, dim3(blocks), dim3(256), 0, m->stream, (KT*)m->kc, (KT*)m->vc, m->L,
-                           m->hkv, m->T, m->hd, upto, m->c.n_kv_heads * m->hd, m->c.tp_rank * m->hkv, seed,
+                           m->B, m->hkv, m->T, m->hd, upto, m->c.n_kv_heads * m->hd, m->c.tp_rank * m->hkv, seed,
                            SLI_SYNTH_C(1.0));
         SLI_HIP(hipGetLastError());
         return SLI_OK;
     }
-    static int get_kv(sli_model* m, int layer, int which, int upto, float* tmp) {
-        const KT* base = (const KT*)(which == 0 ? m->kc : m->vc) + (size_t)layer * m->hkv * m->T * m->hd;
+    static int get_kv(sli_model* m, int seq, int layer, int which, int upto, float* tmp) {
+        const KT* base = (const KT*)(which == 0 ? m->kc : m->vc) + ((size_t)layer * m->B + seq) * m->hkv * m->T * m->hd;
         hipLaunchKernelGGL(get_kv_kernel<KT>, dim3(256), dim3(256), 0, m->stream, base, tmp, m->hkv, m->T, m->hd, upto);
         SLI_HIP(hipGetLastError());
         return SLI_OK;
@@ -395,14 +545,15 @@ static int capture(sli_model* m) {
     return SLI_OK;
 }
 
-static int upload_state(sli_model* m, const DevState& h) {
-    SLI_HIP(hipMemcpyAsync(m->st, &h, sizeof(DevState), hipMemcpyHostToDevice, m->stream));
+static int upload_states(sli_model* m, const std::vector<DevState>& h) {
+    SLI_HIP(hipMemcpyAsync(m->st, h.data(), sizeof(DevState) * m->B, hipMemcpyHostToDevice, m->stream));
     SLI_HIP(hipStreamSynchronize(m->stream));
     return SLI_OK;
 }
 
-static int download_state(sli_model* m, DevState* h) {
-    SLI_HIP(hipMemcpyAsync(h, m->st, sizeof(DevState), hipMemcpyDeviceToHost, m->stream));
+static int download_states(sli_model* m, std::vector<DevState>& h) {
+    h.resize(m->B);
+    SLI_HIP(hipMemcpyAsync(h.data(), m->st, sizeof(DevState) * m->B, hipMemcpyDeviceToHost, m->stream));
     SLI_HIP(hipStreamSynchronize(m->stream));
     return SLI_OK;
 }
@@ -459,6 +610,14 @@ int sli_model_create(const sli_model_config* cfg, const void* comm_id, sli_model
                   ((size_t)(c.dim / c.tp_size) * wb) % 16 == 0,
               SLI_ERR_SHAPE, "row bytes must be multiples of 16");
     SLI_CHECK(c.dim <= kGemvMaxCols && c.ffn / c.tp_size <= kGemvMaxCols, SLI_ERR_SHAPE, "row too long for LDS staging");
+    const int B = c.batch > 0 ? c.batch : 1;
+    SLI_CHECK(B <= kBgMaxBatch, SLI_ERR_SHAPE, "batch must be at most 8");
+    if (B > 1) {
+        SLI_CHECK(c.w_dtype == SLI_DT_F16, SLI_ERR_ARG, "batch > 1 needs fp16 weights (MFMA projections)");
+        SLI_CHECK(c.dim % 32 == 0 && (c.ffn / c.tp_size) % 32 == 0 && ((c.n_heads / c.tp_size) * c.head_dim) % 32 == 0,
+                  SLI_ERR_SHAPE, "batch > 1: projection inputs must be multiples of 32");
+        SLI_CHECK((size_t)B * c.dim <= (size_t)kBgMaxStageElems, SLI_ERR_SHAPE, "batch * dim too large to stage");
+    }
 
     SLI_HIP(hipSetDevice(c.device));
     sli_model* m = new sli_model();
@@ -469,6 +628,7 @@ int sli_model_create(const sli_model_config* cfg, const void* comm_id, sli_model
     };
     if (hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(SLI_ERR_HIP, "hipStreamCreate"));
+    m->B = B;
     m->D = c.dim;
     m->L = c.n_layers;
     m->T = c.max_len;
@@ -507,24 +667,42 @@ int sli_model_create(const sli_model_config* cfg, const void* comm_id, sli_model
             A((void**)&w.down_s, sizeof(float) * D);
         }
     }
-    const size_t kv_elems = (size_t)m->L * m->hkv * m->T * hd;
+    const size_t kv_elems = (size_t)m->L * B * m->hkv * m->T * hd;
     A(&m->kc, kv_elems * m->kvbytes);
     A(&m->vc, kv_elems * m->kvbytes);
-    A((void**)&m->x, sizeof(float) * D);
-    A((void**)&m->xpart, sizeof(float) * D);
-    A((void**)&m->q, sizeof(float) * m->hq * hd);
-    A((void**)&m->attn, sizeof(float) * m->hq * hd);
-    A((void**)&m->act, sizeof(float) * m->Il);
-    A((void**)&m->logits, sizeof(float) * m->v_n);
-    A((void**)&m->part, mha_part_bytes(m->T, m->hq, hd));  // split-context partials
-    A((void**)&m->attn_count, sizeof(unsigned) * m->hkv);   // per-kv-head arrival counters (kept zero)
+    A((void**)&m->x, sizeof(float) * B * D);
+    A((void**)&m->xpart, sizeof(float) * B * D);
+    A((void**)&m->q, sizeof(float) * B * m->hq * hd);
+    A((void**)&m->attn, sizeof(float) * B * m->hq * hd);
+    A((void**)&m->act, sizeof(float) * B * m->Il);
+    A((void**)&m->logits, sizeof(float) * B * m->v_n);
+    A((void**)&m->part, mha_part_bytes(m->T, B * m->hq, hd));  // split-context partials
+    A((void**)&m->attn_count, sizeof(unsigned) * B * m->hkv);   // per-kv-head arrival counters (kept zero)
+    size_t bg_part = 0;
+    int bg_groups = 1;
+    if (B > 1) {  // tilings of the batched projections (bgemm.h)
+        m->bp_qkv = bg_plan(qkv_rows / 16, D, B, true);
+        m->bp_wo = bg_plan((D + 15) / 16, m->hq * hd, B, false);
+        m->bp_gu = bg_plan(m->Il / 8, D, B, true);
+        m->bp_down = bg_plan((D + 15) / 16, m->Il, B, false);
+        m->bp_lm = bg_plan((m->v_n + 15) / 16, D, B, true);
+        for (const BgPlan* p : {&m->bp_qkv, &m->bp_wo, &m->bp_gu, &m->bp_down, &m->bp_lm}) {
+            if (p->groups <= 0) return bail(fail(SLI_ERR_SHAPE, "batched projection: no tiling fits"));
+            bg_part = std::max(bg_part, bg_part_bytes(*p));
+            bg_groups = std::max(bg_groups, p->groups);
+        }
+        m->key_ld = std::max(kGemvMaxBlocks, m->bp_lm.groups);
+        A((void**)&m->bg_ws, bg_part + 256);
+        A((void**)&m->bg_cnt, sizeof(unsigned) * bg_groups);
+    }
+    A((void**)&m->bkeys, sizeof(unsigned long long) * B);
 
     A((void**)&m->sin_t, sizeof(float) * (size_t)m->T * (hd / 2));
     A((void**)&m->cos_t, sizeof(float) * (size_t)m->T * (hd / 2));
-    A((void**)&m->keys, sizeof(unsigned long long) * kGemvMaxBlocks);
-    A((void**)&m->st, sizeof(DevState));
-    A((void**)&m->prompt, sizeof(int32_t) * (m->T + 1));
-    A((void**)&m->hist, sizeof(int32_t) * (m->T + 1));
+    A((void**)&m->keys, sizeof(unsigned long long) * B * m->key_ld);
+    A((void**)&m->st, sizeof(DevState) * B);
+    A((void**)&m->prompt, sizeof(int32_t) * B * (m->T + 1));
+    A((void**)&m->hist, sizeof(int32_t) * B * (m->T + 1));
     if (rc != SLI_OK) return bail(rc);
 
     std::vector<float> s, co;
@@ -532,10 +710,12 @@ int sli_model_create(const sli_model_config* cfg, const void* comm_id, sli_model
     if (hipMemcpy(m->sin_t, s.data(), s.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(m->cos_t, co.data(), co.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
         return bail(fail(SLI_ERR_HIP, "rope table upload"));
-    if (hipMemset(m->prompt, 0, sizeof(int32_t) * (m->T + 1)) != hipSuccess ||
-        hipMemset(m->attn_count, 0, sizeof(unsigned) * m->hkv) != hipSuccess ||
-        hipMemset(m->hist, 0, sizeof(int32_t) * (m->T + 1)) != hipSuccess)
+    if (hipMemset(m->prompt, 0, sizeof(int32_t) * B * (m->T + 1)) != hipSuccess ||
+        hipMemset(m->attn_count, 0, sizeof(unsigned) * B * m->hkv) != hipSuccess ||
+        hipMemset(m->hist, 0, sizeof(int32_t) * B * (m->T + 1)) != hipSuccess ||
+        (m->bg_cnt && hipMemset(m->bg_cnt, 0, sizeof(unsigned) * bg_groups) != hipSuccess))
         return bail(fail(SLI_ERR_HIP, "memset"));
+    if (B > 1 && (rc = SLI_DISPATCH(m, prepare, m)) != SLI_OK) return bail(rc);
     if ((rc = sli_model_reset(m)) != SLI_OK) return bail(rc);
 
     // Debug switches (tests only): SLI_DEBUG_FORCE_COMM=1 runs the tensor-parallel step
@@ -633,12 +813,12 @@ int sli_model_load_flat(sli_model* m, const char* path) {
 int sli_model_reset(sli_model* m) {
     SLI_CHECK(m, SLI_ERR_ARG, "null model");
     SLI_HIP(hipSetDevice(m->c.device));
-    const size_t kv = (size_t)m->L * m->hkv * m->T * m->hd * m->kvbytes;
+    const size_t kv = (size_t)m->L * m->B * m->hkv * m->T * m->hd * m->kvbytes;
     SLI_HIP(hipMemsetAsync(m->kc, 0, kv, m->stream));
     SLI_HIP(hipMemsetAsync(m->vc, 0, kv, m->stream));
-    DevState h{};
-    h.advance = 1;
-    return upload_state(m, h);
+    std::vector<DevState> h(m->B);
+    for (auto& d : h) d.advance = 1;
+    return upload_states(m, h);
 }
 
 int sli_model_fill_kv_synthetic(sli_model* m, uint32_t seed, int32_t upto) {
@@ -651,41 +831,87 @@ int sli_model_fill_kv_synthetic(sli_model* m, uint32_t seed, int32_t upto) {
     return SLI_OK;
 }
 
-int sli_model_set_state(sli_model* m, int32_t token, int32_t pos, int32_t advance) {
+// seq < 0: every sequence
+static int set_state(sli_model* m, int seq, int32_t token, int32_t pos, int32_t advance) {
     SLI_CHECK(m, SLI_ERR_ARG, "null model");
+    SLI_CHECK(seq < m->B, SLI_ERR_RANGE, "sequence index out of range");
     SLI_CHECK(token >= 0 && token < m->V, SLI_ERR_RANGE, "Token index is greater than vocab size.");
     SLI_CHECK(pos >= 0 && pos < m->T, SLI_ERR_RANGE, "position out of range");
-    DevState h{};
-    SLI_TRY(download_state(m, &h));
-    h.token = token;
-    h.pos = pos;
-    h.advance = advance ? 1 : 0;
-    h.key = 0;
-    h.error = 0;
-    SLI_HIP(hipMemcpyAsync(m->hist + pos, &token, sizeof(int32_t), hipMemcpyHostToDevice, m->stream));
-    return upload_state(m, h);
+    std::vector<DevState> h;
+    SLI_TRY(download_states(m, h));
+    for (int b = 0; b < m->B; ++b) {
+        if (seq >= 0 && b != seq) continue;
+        h[b].token = token;
+        h[b].pos = pos;
+        h[b].advance = advance ? 1 : 0;
+        h[b].key = 0;
+        h[b].error = 0;
+        SLI_HIP(hipMemcpyAsync(m->hist + (size_t)b * (m->T + 1) + pos, &token, sizeof(int32_t), hipMemcpyHostToDevice,
+                               m->stream));
+    }
+    return upload_states(m, h);
 }
 
-int sli_model_set_prompt(sli_model* m, const int32_t* ids, int32_t n) {
+static int set_prompt(sli_model* m, int seq, const int32_t* ids, int32_t n) {
     SLI_CHECK(m && ids, SLI_ERR_ARG, "null argument");
+    SLI_CHECK(seq < m->B, SLI_ERR_RANGE, "sequence index out of range");
     SLI_CHECK(n >= 1 && n <= m->T, SLI_ERR_RANGE, "prompt length out of range");
     for (int i = 0; i < n; ++i)
         SLI_CHECK(ids[i] >= 0 && ids[i] < m->V, SLI_ERR_RANGE, "Token index is greater than vocab size.");
-    SLI_HIP(hipMemcpyAsync(m->prompt, ids, sizeof(int32_t) * n, hipMemcpyHostToDevice, m->stream));
-    DevState h{};
-    SLI_TRY(download_state(m, &h));
-    h.n_forced = n;
-    return upload_state(m, h);
+    std::vector<DevState> h;
+    SLI_TRY(download_states(m, h));
+    for (int b = 0; b < m->B; ++b) {
+        if (seq >= 0 && b != seq) continue;
+        SLI_HIP(hipMemcpyAsync(m->prompt + (size_t)b * (m->T + 1), ids, sizeof(int32_t) * n, hipMemcpyHostToDevice,
+                               m->stream));
+        h[b].n_forced = n;
+    }
+    return upload_states(m, h);
+}
+
+static int get_state(sli_model* m, int seq, int32_t* pos, int32_t* token, int32_t* last_argmax, int32_t* error) {
+    SLI_CHECK(m, SLI_ERR_ARG, "null model");
+    SLI_CHECK(seq >= 0 && seq < m->B, SLI_ERR_RANGE, "sequence index out of range");
+    std::vector<DevState> h;
+    SLI_TRY(download_states(m, h));
+    if (pos) *pos = h[seq].pos;
+    if (token) *token = h[seq].token;
+    if (last_argmax) *last_argmax = h[seq].last_argmax;
+    if (error) *error = h[seq].error;
+    return SLI_OK;
+}
+
+int sli_model_set_state(sli_model* m, int32_t token, int32_t pos, int32_t advance) {
+    return set_state(m, -1, token, pos, advance);
+}
+
+int sli_model_set_state_seq(sli_model* m, int32_t seq, int32_t token, int32_t pos, int32_t advance) {
+    SLI_CHECK(seq >= 0, SLI_ERR_RANGE, "sequence index out of range");
+    return set_state(m, seq, token, pos, advance);
+}
+
+int sli_model_set_prompt(sli_model* m, const int32_t* ids, int32_t n) { return set_prompt(m, -1, ids, n); }
+
+int sli_model_set_prompt_seq(sli_model* m, int32_t seq, const int32_t* ids, int32_t n) {
+    SLI_CHECK(seq >= 0, SLI_ERR_RANGE, "sequence index out of range");
+    return set_prompt(m, seq, ids, n);
 }
 
 int sli_model_get_state(sli_model* m, int32_t* pos, int32_t* token, int32_t* last_argmax, int32_t* error) {
-    SLI_CHECK(m, SLI_ERR_ARG, "null model");
-    DevState h{};
-    SLI_TRY(download_state(m, &h));
-    if (pos) *pos = h.pos;
-    if (token) *token = h.token;
-    if (last_argmax) *last_argmax = h.last_argmax;
-    if (error) *error = h.error;
+    return get_state(m, 0, pos, token, last_argmax, error);
+}
+
+int sli_model_get_state_seq(sli_model* m, int32_t seq, int32_t* pos, int32_t* token, int32_t* last_argmax,
+                            int32_t* error) {
+    return get_state(m, seq, pos, token, last_argmax, error);
+}
+
+int sli_model_get_history(sli_model* m, int32_t seq, int32_t n, int32_t* out) {
+    SLI_CHECK(m && out, SLI_ERR_ARG, "null argument");
+    SLI_CHECK(seq >= 0 && seq < m->B && n >= 0 && n <= m->T, SLI_ERR_RANGE, "sequence / length out of range");
+    SLI_HIP(hipMemcpyAsync(out, m->hist + (size_t)seq * (m->T + 1), sizeof(int32_t) * n, hipMemcpyDeviceToHost,
+                           m->stream));
+    SLI_HIP(hipStreamSynchronize(m->stream));
     return SLI_OK;
 }
 
@@ -704,36 +930,56 @@ int sli_model_sync(sli_model* m) {
 
 int sli_model_get_logits(sli_model* m, float* host, int32_t n, int32_t* vocab_lo) {
     SLI_CHECK(m && host, SLI_ERR_ARG, "null argument");
-    SLI_CHECK(n >= m->v_n, SLI_ERR_SHAPE, "host buffer smaller than the local vocab shard");
-    SLI_HIP(hipMemcpyAsync(host, m->logits, sizeof(float) * m->v_n, hipMemcpyDeviceToHost, m->stream));
+    SLI_CHECK(n >= m->B * m->v_n, SLI_ERR_SHAPE, "host buffer smaller than the local vocab shard x batch");
+    SLI_HIP(hipMemcpyAsync(host, m->logits, sizeof(float) * m->B * m->v_n, hipMemcpyDeviceToHost, m->stream));
     SLI_HIP(hipStreamSynchronize(m->stream));
     if (vocab_lo) *vocab_lo = m->v_lo;
+    return SLI_OK;
+}
+
+int sli_model_predict_batch(sli_model* m, const int32_t* prompts, const int32_t* lens, int32_t ld, int32_t max_length,
+                            int32_t* tokens_out, float* logits_out) {
+    SLI_CHECK(m && prompts && lens && tokens_out, SLI_ERR_ARG, "null argument");
+    SLI_CHECK(max_length >= 1 && max_length <= m->T, SLI_ERR_RANGE, "max_length must be in [1, max_len]");
+    for (int b = 0; b < m->B; ++b) {
+        SLI_CHECK(lens[b] >= 1 && lens[b] <= ld, SLI_ERR_RANGE, "prompt length out of range");
+        SLI_TRY(set_prompt(m, b, prompts + (size_t)b * ld, lens[b]));
+        SLI_TRY(set_state(m, b, prompts[(size_t)b * ld], 0, 1));
+    }
+    const size_t per_step = (size_t)m->B * m->v_n;
+    for (int t = 0; t < max_length; ++t) {  // model.cpp:157
+        SLI_TRY(sli_model_step(m));
+        if (logits_out) SLI_TRY(sli_model_get_logits(m, logits_out + (size_t)t * per_step, (int32_t)per_step, nullptr));
+    }
+    for (int b = 0; b < m->B; ++b)
+        SLI_HIP(hipMemcpyAsync(tokens_out + (size_t)b * max_length, m->hist + (size_t)b * (m->T + 1),
+                               sizeof(int32_t) * max_length, hipMemcpyDeviceToHost, m->stream));
+    SLI_HIP(hipStreamSynchronize(m->stream));
     return SLI_OK;
 }
 
 int sli_model_predict(sli_model* m, const int32_t* prompt, int32_t n_prompt, int32_t max_length, int32_t* tokens_out,
                       float* logits_out) {
     SLI_CHECK(m && prompt && tokens_out, SLI_ERR_ARG, "null argument");
-    SLI_CHECK(max_length >= 1 && max_length <= m->T, SLI_ERR_RANGE, "max_length must be in [1, max_len]");
-    SLI_TRY(sli_model_set_prompt(m, prompt, n_prompt));
-    SLI_TRY(sli_model_set_state(m, prompt[0], 0, 1));
-    for (int t = 0; t < max_length; ++t) {  // model.cpp:157
-        SLI_TRY(sli_model_step(m));
-        if (logits_out) SLI_TRY(sli_model_get_logits(m, logits_out + (size_t)t * m->v_n, m->v_n, nullptr));
-    }
-    SLI_HIP(hipMemcpyAsync(tokens_out, m->hist, sizeof(int32_t) * max_length, hipMemcpyDeviceToHost, m->stream));
-    SLI_HIP(hipStreamSynchronize(m->stream));
-    return SLI_OK;
+    SLI_CHECK(n_prompt >= 1, SLI_ERR_RANGE, "prompt length out of range");
+    std::vector<int32_t> ps((size_t)m->B * n_prompt), lens(m->B, n_prompt);
+    for (int b = 0; b < m->B; ++b) std::memcpy(ps.data() + (size_t)b * n_prompt, prompt, sizeof(int32_t) * n_prompt);
+    return sli_model_predict_batch(m, ps.data(), lens.data(), n_prompt, max_length, tokens_out, logits_out);
 }
 
 int sli_model_get_kv(sli_model* m, int32_t layer, int32_t which, int32_t upto, float* host) {
+    return sli_model_get_kv_seq(m, 0, layer, which, upto, host);
+}
+
+int sli_model_get_kv_seq(sli_model* m, int32_t seq, int32_t layer, int32_t which, int32_t upto, float* host) {
     SLI_CHECK(m && host, SLI_ERR_ARG, "null argument");
-    SLI_CHECK(layer >= 0 && layer < m->L && upto > 0 && upto <= m->T && (which == 0 || which == 1), SLI_ERR_RANGE,
-              "layer/which/upto out of range");
+    SLI_CHECK(layer >= 0 && layer < m->L && upto > 0 && upto <= m->T && (which == 0 || which == 1) && seq >= 0 &&
+                  seq < m->B,
+              SLI_ERR_RANGE, "seq/layer/which/upto out of range");
     const size_t n = (size_t)upto * m->hkv * m->hd;
     float* tmp = nullptr;
     SLI_HIP(hipMalloc(&tmp, n * 4));
-    int rc = SLI_DISPATCH(m, get_kv, m, layer, which, upto, tmp);
+    int rc = SLI_DISPATCH(m, get_kv, m, seq, layer, which, upto, tmp);
     if (rc == SLI_OK && hipMemcpyAsync(host, tmp, n * 4, hipMemcpyDeviceToHost, m->stream) != hipSuccess)
         rc = fail(SLI_ERR_HIP, "copy kv");
     if (hipStreamSynchronize(m->stream) != hipSuccess && rc == SLI_OK) rc = fail(SLI_ERR_HIP, "sync");
@@ -805,14 +1051,16 @@ int sli_model_stream(sli_model* m, sli_stream_t* out) {
 
 int sli_model_step_bytes(sli_model* m, double* weight_bytes, double* kv_bytes) {
     SLI_CHECK(m, SLI_ERR_ARG, "null model");
-    DevState h{};
-    SLI_TRY(download_state(m, &h));
+    std::vector<DevState> h;
+    SLI_TRY(download_states(m, h));
     const double wb = (double)m->wbytes, D = m->D, hd = m->hd;
     const double per_layer = ((m->hq + 2.0 * m->hkv) * hd * D + D * m->hq * hd + 3.0 * m->Il * D) * wb;
     double w = m->L * per_layer + (double)m->v_n * D * wb;
     if (m->c.w_dtype == SLI_DT_I8) w += 4.0 * (m->L * ((m->hq + 2.0 * m->hkv) * hd + 2.0 * D + 2.0 * m->Il) + m->v_n);
     if (weight_bytes) *weight_bytes = w;
-    if (kv_bytes) *kv_bytes = 2.0 * m->L * (h.pos + 1.0) * m->hkv * hd * (double)m->kvbytes;
+    double ctx = 0.0;
+    for (const DevState& d : h) ctx += d.pos + 1.0;
+    if (kv_bytes) *kv_bytes = 2.0 * m->L * ctx * m->hkv * hd * (double)m->kvbytes;
     return SLI_OK;
 }
 
@@ -822,8 +1070,8 @@ int sli_model_time_gemv(sli_model* m, int32_t iters, double* avg_us, double* byt
     SLI_HIP(hipSetDevice(m->c.device));
     // the probe re-runs the step's GEMVs in place: save and restore the residual stream
     float* xsave = nullptr;
-    SLI_HIP(hipMalloc(&xsave, sizeof(float) * m->D));
-    SLI_HIP(hipMemcpyAsync(xsave, m->x, sizeof(float) * m->D, hipMemcpyDeviceToDevice, m->stream));
+    SLI_HIP(hipMalloc(&xsave, sizeof(float) * m->B * m->D));
+    SLI_HIP(hipMemcpyAsync(xsave, m->x, sizeof(float) * m->B * m->D, hipMemcpyDeviceToDevice, m->stream));
     hipEvent_t e0, e1;
     SLI_HIP(hipEventCreate(&e0));
     SLI_HIP(hipEventCreate(&e1));
@@ -834,7 +1082,7 @@ int sli_model_time_gemv(sli_model* m, int32_t iters, double* avg_us, double* byt
     SLI_HIP(hipEventSynchronize(e1));
     float ms = 0.0f;
     SLI_HIP(hipEventElapsedTime(&ms, e0, e1));
-    SLI_HIP(hipMemcpyAsync(m->x, xsave, sizeof(float) * m->D, hipMemcpyDeviceToDevice, m->stream));
+    SLI_HIP(hipMemcpyAsync(m->x, xsave, sizeof(float) * m->B * m->D, hipMemcpyDeviceToDevice, m->stream));
     SLI_HIP(hipStreamSynchronize(m->stream));
     (void)hipFree(xsave);
     (void)hipEventDestroy(e0);

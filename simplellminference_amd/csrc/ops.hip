@@ -4,6 +4,7 @@
 #include <vector>
 
 #include "attention.h"
+#include "bgemm.h"
 #include "common.h"
 #include "gemv.h"
 #include "ops_internal.h"
@@ -162,13 +163,14 @@ int attn_wg_positions(int kv_dtype, int head_dim) {
 template <typename KT, int HD>
 static int mha_launch_hd(const float* q, const KT* kc, const KT* vc, float* out, int layer, int pos, const int32_t* pos_dev,
                          int T, int H, int Hkv, long long pos_stride, long long head_stride, long long layer_stride,
-                         float* part, unsigned* counters, hipStream_t s) {
+                         float* part, unsigned* counters, hipStream_t s, int seq_heads, int pos_seq_stride) {
     using Geo = AttnGeom<KT, HD>;
     constexpr int ppw_wg = Geo::PPWG;
     const int wg_splits = (T + ppw_wg - 1) / ppw_wg;
     if (wg_splits > kAttnMaxWgSplits) return fail(SLI_ERR_SHAPE, "mha: context too long for the split merge");
     AttnArgs<KT> a{q,    kc + (long long)layer * layer_stride, vc + (long long)layer * layer_stride, pos_stride,
-                   head_stride, part, out, counters, pos_dev, pos, Hkv, wg_splits, 1.0f / sqrtf((float)HD)};
+                   head_stride, part, out, counters, pos_dev, pos, Hkv, wg_splits, 1.0f / sqrtf((float)HD),
+                   seq_heads > 0 ? seq_heads : Hkv, pos_seq_stride};
     const int blocks = Hkv * wg_splits;
     const int g = H / Hkv;
     switch (g) {
@@ -185,20 +187,21 @@ static int mha_launch_hd(const float* q, const KT* kc, const KT* vc, float* out,
 template <typename KT>
 int mha_launch(const float* q, const KT* kc, const KT* vc, float* out, int layer, int pos, const int32_t* pos_dev,
                int T, int hd, int H, int Hkv, long long pos_stride, long long head_stride, long long layer_stride,
-               float* part, unsigned* counters, hipStream_t s) {
+               float* part, unsigned* counters, hipStream_t s, int seq_heads, int pos_seq_stride) {
     if (hd == 128)
         return mha_launch_hd<KT, 128>(q, kc, vc, out, layer, pos, pos_dev, T, H, Hkv, pos_stride, head_stride,
-                                      layer_stride, part, counters, s);
+                                      layer_stride, part, counters, s, seq_heads, pos_seq_stride);
     if (hd == 64)
         return mha_launch_hd<KT, 64>(q, kc, vc, out, layer, pos, pos_dev, T, H, Hkv, pos_stride, head_stride,
-                                     layer_stride, part, counters, s);
+                                     layer_stride, part, counters, s, seq_heads, pos_seq_stride);
     return fail(SLI_ERR_SHAPE, "mha: head_dim must be 64 or 128");
 }
 
 template int mha_launch<float>(const float*, const float*, const float*, float*, int, int, const int32_t*, int, int,
-                               int, int, long long, long long, long long, float*, unsigned*, hipStream_t);
+                               int, int, long long, long long, long long, float*, unsigned*, hipStream_t, int, int);
 template int mha_launch<__half>(const float*, const __half*, const __half*, float*, int, int, const int32_t*, int,
-                                int, int, int, long long, long long, long long, float*, unsigned*, hipStream_t);
+                                int, int, int, long long, long long, long long, float*, unsigned*, hipStream_t, int,
+                                int);
 
 size_t mha_part_bytes(int T, int H, int hd) {
     const int ppw_wg_min = attn_wg_positions(SLI_DT_F32, hd);
@@ -246,6 +249,31 @@ int sli_matmul(const float* x, const void* w, int w_dtype, const float* w_row_sc
             return matmul_dispatch<int8_t>(x, (const int8_t*)w, w_row_scale, y, rows, cols, scale, s);
         default: return fail(SLI_ERR_ARG, "sli_matmul: bad dtype");
     }
+}
+
+size_t sli_matmul_batch_workspace_bytes(int32_t rows, int32_t cols, int32_t batch) {
+    if (rows <= 0 || cols <= 0 || batch <= 0 || batch > kBgMaxBatch || cols % 32 != 0) return 0;
+    return bg_ws_bytes(bg_plan((rows + 15) / 16, cols, batch, false));
+}
+
+int sli_matmul_batch(const float* x, const void* w, int w_dtype, float* y, int32_t rows, int32_t cols, int32_t batch,
+                     void* workspace, size_t workspace_bytes, sli_stream_t stream) {
+    SLI_CHECK(x && w && y && workspace, SLI_ERR_ARG, "sli_matmul_batch: null pointer");
+    SLI_CHECK(w_dtype == SLI_DT_F16, SLI_ERR_ARG, "sli_matmul_batch: fp16 weights only");
+    SLI_CHECK(rows > 0 && cols > 0 && cols % 32 == 0, SLI_ERR_SHAPE, "sli_matmul_batch: cols must be a multiple of 32");
+    SLI_CHECK(batch >= 1 && batch <= kBgMaxBatch, SLI_ERR_SHAPE, "sli_matmul_batch: batch must be in [1, 8]");
+    SLI_CHECK((uintptr_t)x % 16 == 0 && (uintptr_t)w % 16 == 0, SLI_ERR_ARG, "sli_matmul_batch: 16-byte alignment");
+    const BgPlan p = bg_plan((rows + 15) / 16, cols, batch, false);
+    SLI_CHECK(p.groups > 0, SLI_ERR_SHAPE, "sli_matmul_batch: no tiling fits");
+    SLI_CHECK(workspace_bytes >= bg_ws_bytes(p), SLI_ERR_ARG, "sli_matmul_batch: workspace too small");
+    hipStream_t s = as_stream(stream);
+    unsigned* cnt = (unsigned*)((char*)workspace + bg_part_bytes(p));
+    SLI_HIP(hipMemsetAsync(cnt, 0, sizeof(unsigned) * p.groups, s));
+    SLI_HIP((bg_allow_lds<BgEpiStore, false>()));
+    BgIn in{x, nullptr, 0.0f, cols, batch, 0, 0, 0, (float*)workspace, cnt};
+    BgEpiStore e{y, nullptr, nullptr, 1.0f, rows, rows};
+    SLI_HIP(launch_bgemm((const __half*)w, in, e, p, s));
+    return SLI_OK;
 }
 
 int sli_rmsnorm(const float* x, const float* w, float* y, int32_t dim, float eps, sli_stream_t stream) {

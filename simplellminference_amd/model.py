@@ -57,7 +57,7 @@ class LlamaModel:
     def __init__(self, tokenizer_path: str = "", model_path: str = "", device_type: str = "cuda",
                  config: LlamaModelConfig | None = None, w_dtype: str = "f16", kv_dtype: str = "f16",
                  act_mode: int = 0, tp_rank: int = 0, tp_size: int = 1, comm_id: bytes | None = None,
-                 device: int = 0, seed: int | None = None):
+                 device: int = 0, seed: int | None = None, batch: int = 1):
         if device_type not in ("cuda", "hip"):
             raise ValueError("Device Type ERROR!")  # op/*.cpp dispatch: only the HIP backend exists here
         self.tokenizer_path = tokenizer_path
@@ -70,6 +70,7 @@ class LlamaModel:
         self.comm_id = comm_id
         self.device = device
         self.seed = seed
+        self.batch = batch  # sequences decoding in lockstep (extension: the reference is batch 1)
         self._h = None
 
     # ------------------------------------------------------------------ model.h:63-67
@@ -79,7 +80,8 @@ class LlamaModel:
             raise ValueError("kv_hidden_size must equal num_key_value_heads * head_dim")
         mc = ModelConfig(c.vocab_size, c.hidden_size, c.num_attention_heads, c.num_key_value_heads, c.head_dim,
                          c.intermediate_size, c.num_hidden_layers, c.max_length, c.rms_norm_eps, c.rope_theta,
-                         self.w_dtype, self.kv_dtype, self.act_mode, self.tp_rank, self.tp_size, self.device)
+                         self.w_dtype, self.kv_dtype, self.act_mode, self.tp_rank, self.tp_size, self.device,
+                         self.batch)
         h = ctypes.c_void_p()
         cid = ctypes.create_string_buffer(self.comm_id, len(self.comm_id)) if self.comm_id else None
         call("sli_model_create", ctypes.byref(mc), cid, ctypes.byref(h))
@@ -121,10 +123,23 @@ class LlamaModel:
         a = np.ascontiguousarray(ids, np.int32)
         call("sli_model_set_prompt", self._h, a.ctypes.data_as(ctypes.c_void_p), a.size)
 
-    def state(self):
+    def state(self, seq: int = 0):
         p, t, a, e = (ctypes.c_int32() for _ in range(4))
-        call("sli_model_get_state", self._h, ctypes.byref(p), ctypes.byref(t), ctypes.byref(a), ctypes.byref(e))
+        call("sli_model_get_state_seq", self._h, seq, ctypes.byref(p), ctypes.byref(t), ctypes.byref(a),
+             ctypes.byref(e))
         return {"pos": p.value, "token": t.value, "last_argmax": a.value, "error": e.value}
+
+    def set_state_seq(self, seq: int, token: int, pos: int, advance: bool = True):
+        call("sli_model_set_state_seq", self._h, seq, token, pos, 1 if advance else 0)
+
+    def set_prompt_seq(self, seq: int, ids):
+        a = np.ascontiguousarray(ids, np.int32)
+        call("sli_model_set_prompt_seq", self._h, seq, a.ctypes.data_as(ctypes.c_void_p), a.size)
+
+    def history(self, seq: int, n: int) -> np.ndarray:
+        out = np.empty(n, np.int32)
+        call("sli_model_get_history", self._h, seq, n, out.ctypes.data_as(ctypes.c_void_p))
+        return out
 
     @property
     def local_vocab(self) -> int:
@@ -140,16 +155,24 @@ class LlamaModel:
         call("sli_model_sync", self._h)
 
     def logits(self) -> tuple[np.ndarray, int]:
-        out = np.empty(self.local_vocab, np.float32)
+        """This rank's vocab shard of the last step's logits: [local vocab], or [batch, local vocab]."""
+        out = np.empty(self.batch * self.local_vocab, np.float32)
         lo = ctypes.c_int32()
         call("sli_model_get_logits", self._h, out.ctypes.data_as(ctypes.c_void_p), out.size, ctypes.byref(lo))
-        return out, lo.value
+        return (out.reshape(self.batch, -1) if self.batch > 1 else out), lo.value
 
     def forward(self, token: int, pos: int) -> np.ndarray:
         """One decode step at (token, pos); returns this rank's logits shard."""
         self.set_state(token, pos, advance=False)
         self.step()
         return self.logits()[0]
+
+    def forward_batch(self, tokens, positions) -> np.ndarray:
+        """One decode step of every sequence b at (tokens[b], positions[b]); returns [batch, local vocab]."""
+        for b in range(self.batch):
+            self.set_state_seq(b, int(tokens[b]), int(positions[b]), advance=False)
+        self.step()
+        return self.logits()[0].reshape(self.batch, -1)
 
     # ------------------------------------------------------------------ model.cpp:142-187
     def predict(self, prompt_ids, max_length: int, want_logits: bool = False):
@@ -159,6 +182,23 @@ class LlamaModel:
         call("sli_model_predict", self._h, p.ctypes.data_as(ctypes.c_void_p), p.size, max_length,
              toks.ctypes.data_as(ctypes.c_void_p), logits.ctypes.data_as(ctypes.c_void_p) if want_logits else None)
         return (toks, logits) if want_logits else toks
+
+    def predict_batch(self, prompts, max_length: int, want_logits: bool = False):
+        """predict for `batch` sequences with their own prompts (ragged lengths allowed): tokens [batch,
+        max_length] (the token fed at each position), logits [batch, max_length, local vocab]."""
+        if len(prompts) != self.batch:
+            raise ValueError(f"need {self.batch} prompts")
+        ld = max(len(p) for p in prompts)
+        P = np.zeros((self.batch, ld), np.int32)
+        for b, p in enumerate(prompts):
+            P[b, :len(p)] = p
+        lens = np.array([len(p) for p in prompts], np.int32)
+        toks = np.empty((self.batch, max_length), np.int32)
+        logits = np.empty((max_length, self.batch, self.local_vocab), np.float32) if want_logits else None
+        call("sli_model_predict_batch", self._h, P.ctypes.data_as(ctypes.c_void_p), lens.ctypes.data_as(ctypes.c_void_p),
+             ld, max_length, toks.ctypes.data_as(ctypes.c_void_p),
+             logits.ctypes.data_as(ctypes.c_void_p) if want_logits else None)
+        return (toks, logits.transpose(1, 0, 2).copy()) if want_logits else toks
 
     def weight_shard(self, kind: int, index: int = 0) -> np.ndarray:
         """This rank's shard of a weight (sli_tp_plan window) read back as fp32."""
@@ -173,10 +213,10 @@ class LlamaModel:
         call("sli_model_get_weight", self._h, kind, index, out.ctypes.data_as(ctypes.c_void_p), out.size)
         return out
 
-    def kv(self, layer: int, which: int, upto: int) -> np.ndarray:
+    def kv(self, layer: int, which: int, upto: int, seq: int = 0) -> np.ndarray:
         c = self.config
         out = np.empty((upto, c.num_key_value_heads // self.tp_size * c.head_dim), np.float32)
-        call("sli_model_get_kv", self._h, layer, which, upto, out.ctypes.data_as(ctypes.c_void_p))
+        call("sli_model_get_kv_seq", self._h, seq, layer, which, upto, out.ctypes.data_as(ctypes.c_void_p))
         return out
 
     # ------------------------------------------------------------------ measurement

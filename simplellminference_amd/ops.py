@@ -41,6 +41,23 @@ def matmul(x, w, y=None, scale: float = 1.0, row_scale=None):
     return y
 
 
+def matmul_batch(x, w, y=None):
+    """Batched projection for B <= 8 sequences on MFMA (bgemm.h): y[b] = W @ x[b]; x [B, cols] fp32, W
+    [rows, cols] fp16, y [B, rows] fp32. No reference counterpart (the reference is batch 1)."""
+    batch, cols = x.shape
+    rows = w.shape[0]
+    if w.shape[1] != cols:
+        raise ValueError("Tensor with Wrong Dim!")
+    y = torch.empty(batch, rows, device=x.device, dtype=torch.float32) if y is None else y
+    nbytes = _lib.load().sli_matmul_batch_workspace_bytes(rows, cols, batch)
+    if nbytes == 0:
+        raise ValueError("unsupported batched shape (cols % 32 != 0 or batch > 8)")
+    ws = torch.empty(nbytes // 4 + 1, device=x.device, dtype=torch.float32)
+    _dev(x, w, y, ws)
+    call("sli_matmul_batch", _p(x), _p(w), _DT[w.dtype], _p(y), rows, cols, batch, _p(ws), ws.numel() * 4, _s())
+    return y
+
+
 def rmsnorm(x, w, eps: float, y=None):
     """rmsnorm_kernel_cuda (rms_kernel.cuh:6-7)."""
     y = torch.empty_like(x) if y is None else y

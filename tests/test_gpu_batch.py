@@ -1,0 +1,150 @@
+"""Batched decode (B sequences decoding in lockstep, projections on MFMA in
+bgemm.h) against the C oracle run once per sequence on identical synthetic weights and prompts.
+
+Bar: per-sequence greedy token ids bit-exact; logits within the north_star tolerance 1e-3 (fp16 weights:
+the oracle computes in fp32 on the identically rounded weights and the same fp16 K/V rounding). The
+batched projection itself is held to 1e-4 (relative + absolute) against a float64 product of the same
+fp16 weights, and is bit-exact on small-integer data (exact in fp16 and fp32).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+PROMPTS = [[1, 17, 42, 99], [5, 6], [300, 2, 77, 8, 9], [11]]  # ragged prompts, one per sequence
+
+
+def _t(torch, a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def _ocfg(oracle, cfg):
+    return oracle.Config(cfg.vocab_size, cfg.hidden_size, cfg.num_attention_heads, cfg.num_key_value_heads,
+                         cfg.head_dim, cfg.intermediate_size, cfg.num_hidden_layers, cfg.max_length,
+                         cfg.rms_norm_eps, cfg.rope_theta)
+
+
+@pytest.mark.parametrize("rows,cols,batch", [(4096, 4096, 8), (768, 4096, 8), (4096, 14336, 8), (4096, 512, 8),
+                                             (16032, 4096, 8), (100, 256, 3), (4000, 4096, 5), (16, 32, 1),
+                                             (6144, 4096, 2)])
+def test_matmul_batch_f16(gpu, rows, cols, batch):
+    torch = gpu
+    from simplellminference_amd import ops
+    r = np.random.default_rng(rows + cols + batch)
+    x = r.standard_normal((batch, cols)).astype(np.float32)
+    w16 = (r.standard_normal((rows, cols)) / np.sqrt(cols)).astype(np.float16)
+    want = x.astype(np.float64) @ w16.astype(np.float64).T
+    got = ops.matmul_batch(_t(torch, x), _t(torch, w16)).cpu().numpy()
+    err = np.abs(got - want)
+    assert np.all(err <= 1e-4 + 1e-4 * np.abs(want)), err.max()
+
+
+@pytest.mark.parametrize("rows,cols,batch", [(64, 128, 8), (48, 4096, 7), (4096, 1024, 8)])
+def test_matmul_batch_exact_integers(gpu, rows, cols, batch):
+    """Small integers are exact in fp16 (weights, hi part; lo = 0) and their sums exact in fp32, so any
+    fragment-layout, tile-map or split-merge error shows as a mismatch."""
+    torch = gpu
+    from simplellminference_amd import ops
+    r = np.random.default_rng(7 + rows)
+    x = r.integers(-3, 4, (batch, cols)).astype(np.float32)
+    w = r.integers(-3, 4, (rows, cols)).astype(np.float16)
+    want = (x.astype(np.int64) @ w.astype(np.int64).T).astype(np.float32)
+    got = ops.matmul_batch(_t(torch, x), _t(torch, w)).cpu().numpy()
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("name", ["tiny", "tiny-gqa"])
+@pytest.mark.parametrize("kv", ["f16", "f32"])
+def test_batch_predict_parity(gpu, oracle, name, kv):
+    from simplellminference_amd.model import LlamaModel, preset
+    cfg = preset(name)
+    gm = LlamaModel(config=cfg, w_dtype="f16", kv_dtype=kv, seed=0, batch=len(PROMPTS)).init()
+    steps = 36  # BASELINE.json configs[0]: prompt + greedy, 36 positions
+    toks, logits = gm.predict_batch(PROMPTS, steps, want_logits=True)
+    gm.close()
+    for b, p in enumerate(PROMPTS):
+        om = oracle.Model(_ocfg(oracle, cfg), seed=0, wmode=oracle.W_F16, kv_f16=(kv == "f16"))
+        otok, olog = om.predict(p, steps)
+        om.close()
+        assert np.array_equal(toks[b], otok), (b, toks[b], otok)
+        assert np.abs(logits[b] - olog).max() <= 1e-3, (b, np.abs(logits[b] - olog).max())
+
+
+def test_batch_state_and_history(gpu, oracle):
+    """Per-sequence state after a batched predict: positions advance together, last_argmax is each
+    sequence's own greedy choice, history is the fed tokens, KV rows match the oracle's."""
+    from simplellminference_amd.model import LlamaModel, preset
+    cfg = preset("tiny-gqa")
+    gm = LlamaModel(config=cfg, w_dtype="f16", kv_dtype="f16", seed=0, batch=len(PROMPTS)).init()
+    toks, logits = gm.predict_batch(PROMPTS, 12, want_logits=True)
+    for b, p in enumerate(PROMPTS):
+        st = gm.state(b)
+        assert st["pos"] == 12 and st["error"] == 0
+        assert st["last_argmax"] == int(np.argmax(logits[b, -1]))
+        assert np.array_equal(gm.history(b, 12), toks[b])
+        om = oracle.Model(_ocfg(oracle, cfg), seed=0, wmode=oracle.W_F16, kv_f16=True)
+        om.predict(p, 12)
+        ok, ov = om.kv_cache()
+        for layer in range(cfg.num_hidden_layers):
+            np.testing.assert_allclose(gm.kv(layer, 0, 12, seq=b), ok[layer, :12], rtol=0, atol=2e-3)
+            np.testing.assert_allclose(gm.kv(layer, 1, 12, seq=b), ov[layer, :12], rtol=0, atol=2e-3)
+        om.close()
+    gm.close()
+
+
+def test_batch_tp_step_on_one_rank_communicator(gpu, oracle, monkeypatch):
+    """SLI_DEBUG_FORCE_COMM with a batch: partials, the [B][D] RCCL sum all-reduces and the [B] uint64 MAX
+    argmax all-reduce, all captured in the step graph."""
+    from simplellminference_amd.model import LlamaModel, preset
+    monkeypatch.setenv("SLI_DEBUG_FORCE_COMM", "1")
+    cfg = preset("tiny-gqa")
+    prompts = PROMPTS[:2]
+    gm = LlamaModel(config=cfg, w_dtype="f16", kv_dtype="f16", seed=0, batch=2).init()
+    toks, logits = gm.predict_batch(prompts, 24, want_logits=True)
+    gm.close()
+    for b, p in enumerate(prompts):
+        om = oracle.Model(_ocfg(oracle, cfg), seed=0, wmode=oracle.W_F16, kv_f16=True)
+        otok, olog = om.predict(p, 24)
+        om.close()
+        assert np.array_equal(toks[b], otok)
+        assert np.abs(logits[b] - olog).max() <= 1e-3
+
+
+def test_llama3_8b_shape_two_layers_batch8(gpu, oracle):
+    """Llama-3-8B layer shapes (D 4096, GQA 32/8, I 14336, vocab 128256, theta 5e5) at ctx 4096, batch 8,
+    two layers; sequence b's KV filled with seed 7 + b to its own (ragged) position, one step each."""
+    from simplellminference_amd.model import LlamaModel, preset
+    cfg = preset("llama3-8b", num_hidden_layers=2)
+    gm = LlamaModel(config=cfg, w_dtype="f16", kv_dtype="f16", seed=1, batch=8).init()
+    gm.fill_kv_synthetic(7, 4095)
+    tokens = [1234 + 9001 * b for b in range(8)]
+    positions = [4095, 4095, 100, 2047, 4000, 1, 3333, 4095]
+    got = gm.forward_batch(tokens, positions)
+    gm.close()
+    om = oracle.Model(_ocfg(oracle, cfg), seed=1, wmode=oracle.W_F16, kv_f16=True)
+    for b in range(8):
+        om.fill_kv_synthetic(7 + b, 4095)
+        want = om.forward(tokens[b], positions[b])
+        assert np.abs(got[b] - want).max() <= 1e-3, (b, np.abs(got[b] - want).max())
+        assert int(np.argmax(got[b])) == int(np.argmax(want))
+    om.close()
+
+
+def test_llama3_8b_full_batch8_properties(gpu):
+    """The C4 workload at TP 1 (32 layers, batch 8, ctx 4096): deterministic idempotent step, finite
+    logits, per-sequence argmax state, algorithmic bytes = SURVEY.md §8(d) (15.009 GB weights, 4.295 GB
+    KV)."""
+    from simplellminference_amd.model import LlamaModel, preset
+    gm = LlamaModel(config=preset("llama3-8b"), w_dtype="f16", kv_dtype="f16", seed=1, batch=8).init()
+    gm.fill_kv_synthetic(7, 4095)
+    tokens = [100 + 17 * b for b in range(8)]
+    a = gm.forward_batch(tokens, [4095] * 8)
+    b = gm.forward_batch(tokens, [4095] * 8)
+    assert np.isfinite(a).all()
+    assert np.array_equal(a, b)
+    for s in range(8):
+        st = gm.state(s)
+        assert st["last_argmax"] == int(np.argmax(a[s])) and st["error"] == 0
+    wb, kb = gm.step_bytes()
+    assert abs(wb - 15.009e9) / 15.009e9 < 0.01 and abs(kb - 4.295e9) / 4.295e9 < 0.01
+    gm.close()
