@@ -33,7 +33,7 @@ constexpr int kBgThreads = 1024;
 constexpr int kBgWaves = kBgThreads / 64;
 constexpr int kBgMaxBatch = 8;
 constexpr int kBgNH = 4;               // staged half-slots (8 k of one sequence) per thread
-constexpr int kBgMaxStageElems = kBgNH * kBgThreads * 8;  // B * (staged k) <= 32768
+constexpr int kBgMaxStageK = kBgNH * (kBgThreads / kBgMaxBatch) * 8;  // staged k per sequence <= 4096
 constexpr int kBgScratch = 1024;       // bytes: ss partials [16][8] f32, inv [8] f32, keys [8] u64, flag
 constexpr int kBgKeysOff = 640;
 constexpr int kBgFlagOff = 704;
@@ -52,6 +52,7 @@ struct BgIn {
     int splits;           // k-ranges (workgroups per tile group)
     float* ws;            // splits > 1: partials [ntiles][splits][16][8]
     unsigned* counters;   // splits > 1: [groups] arrival counters, zero between launches
+    unsigned long long* stamps = nullptr;  // diagnostic (tools/bgemm_lab): per-workgroup s_memrealtime x4
 };
 
 // ---------------------------------------------------------------- host-side plan
@@ -77,7 +78,7 @@ inline BgPlan bg_plan(int ntiles, int K, int B, bool norm, int cus = 256) {
     for (int s = 1; s <= 16; ++s) {
         if (s > 1 && nkb / s < kBgWaves) break;  // every wave keeps at least one block per tile
         const int kbs = (nkb + s - 1) / s;
-        if ((size_t)B * kbs * 32 > (size_t)kBgMaxStageElems) continue;  // staging registers
+        if (kbs * 32 > kBgMaxStageK) continue;  // staging registers
         for (int tpw = 1; tpw <= 64; ++tpw) {
             if (bg_lds_bytes(K, s, tpw) > (size_t)kBgLdsMax) break;
             const int groups = (ntiles + tpw - 1) / tpw;
@@ -165,17 +166,21 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
     const int nsteps = ntg * cpt;
 
     if (tid < kBgMaxBatch) keys[tid] = 0ull;
+    const unsigned long long t_entry = in.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
 
-    // ---- 1. activation staging loads, issued first (s_waitcnt vmcnt counts in issue order)
-    const int n8 = NORM ? (K >> 3) : (nkbs << 2);  // half-slots per sequence in the staged range
+    // ---- 1. activation staging loads, issued first (s_waitcnt vmcnt counts in issue order). Thread t
+    // stages sequence b = t & 7 at the 8-k groups (t >> 3) + 128 n: the 8 lanes of a group write 8
+    // consecutive 16-byte image slots (conflict-free ds_write_b128), the loads stay 32 B per lane.
+    const int n8 = NORM ? (K >> 3) : (nkbs << 2);  // 8-k groups per sequence in the staged range
     const int k8_0 = NORM ? 0 : (kb0 << 2);
-    const int nhs = B * n8;
+    const int sb = tid & (kBgMaxBatch - 1);
+    const bool seq_live = sb < B;
+    const int sbc = min(sb, B - 1);
     float4 xa[kBgNH][2], xw[kBgNH][2];
 #pragma unroll
     for (int n = 0; n < kBgNH; ++n) {
-        const int h = min(tid + n * kBgThreads, nhs - 1);  // clamp, never branch around a load
-        const int b = h / n8, k8 = k8_0 + (h - b * n8);
-        const float4* xp = reinterpret_cast<const float4*>(in.x + (size_t)b * K + (size_t)k8 * 8);
+        const int k8 = k8_0 + min((tid >> 3) + n * (kBgThreads / kBgMaxBatch), n8 - 1);  // clamp, never branch
+        const float4* xp = reinterpret_cast<const float4*>(in.x + (size_t)sbc * K + (size_t)k8 * 8);
         xa[n][0] = xp[0];
         xa[n][1] = xp[1];
         if constexpr (NORM) {
@@ -192,6 +197,15 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
     auto load_step = [&](int k, u32x4(&w)[kBgU]) {
         const int kk = min(k, nsteps - 1);
         const int j = kk / cpt, c = kk - j * cpt;
+#ifdef BG_CONTIG  // timing experiment only (wrong math): the same bytes as lane-contiguous 1 KiB pieces
+        const char* tb = reinterpret_cast<const char*>(W) + (size_t)(t0 + j) * 16 * row_bytes +
+                         (size_t)wave * (16 * row_bytes / kBgWaves);
+#pragma unroll
+        for (int u = 0; u < kBgU; ++u) {
+            const int pc = min(c * kBgU + u, max(wnb - 1, 0));
+            w[u] = load16<true>(tb + ((size_t)pc * 64 + lane) * 16);
+        }
+#else
         const int row = epi.row(t0 + j, lane & 15);
         const char* base = reinterpret_cast<const char*>(W) + (size_t)row * row_bytes + (size_t)q8 * 2;
 #pragma unroll
@@ -199,21 +213,20 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
             const int bi = wb0 + min(c * kBgU + u, max(wnb - 1, 0));
             w[u] = load16<true>(base + (size_t)bi * 64);
         }
+#endif
     };
     u32x4 wa[kBgU], wb[kBgU];
+#ifndef BG_LATE_W
     load_step(0, wa);
     load_step(1, wb);
     __builtin_amdgcn_sched_barrier(0);
+#endif
 
     // ---- 3. per-sequence RMS over the full K (rms_kernel.cpp:12-19)
     if constexpr (NORM) {
-        float ssb[kBgMaxBatch];
-#pragma unroll
-        for (int b = 0; b < kBgMaxBatch; ++b) ssb[b] = 0.0f;
+        float ss = 0.0f;
 #pragma unroll
         for (int n = 0; n < kBgNH; ++n) {
-            const int h = tid + n * kBgThreads;
-            const int b = min(h, nhs - 1) / n8;
             float v = 0.0f;
             v += xa[n][0].x * xa[n][0].x;
             v += xa[n][0].y * xa[n][0].y;
@@ -223,15 +236,11 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
             v += xa[n][1].y * xa[n][1].y;
             v += xa[n][1].z * xa[n][1].z;
             v += xa[n][1].w * xa[n][1].w;
-            v = h < nhs ? v : 0.0f;
-#pragma unroll
-            for (int bb = 0; bb < kBgMaxBatch; ++bb) ssb[bb] += bb == b ? v : 0.0f;
+            ss += ((tid >> 3) + n * (kBgThreads / kBgMaxBatch) < n8) ? v : 0.0f;
         }
 #pragma unroll
-        for (int bb = 0; bb < kBgMaxBatch; ++bb) {
-            const float t = wave_sum(ssb[bb]);
-            if (lane == 0) red[wave * 8 + bb] = t;
-        }
+        for (int o = 8; o < 64; o <<= 1) ss += __shfl_xor(ss, o, kWave);  // lanes of one sequence
+        if (lane < kBgMaxBatch) red[wave * 8 + lane] = ss;
         __syncthreads();
         if (tid < B) {
             float t = 0.0f;
@@ -246,15 +255,13 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
     // ---- 4. the split's k-range of every sequence into LDS as B fragments (hi: column b, lo: 8 + b)
 #pragma unroll
     for (int n = 0; n < kBgNH; ++n) {
-        const int h = tid + n * kBgThreads;
-        const int hc = min(h, nhs - 1);
-        const int b = hc / n8, k8 = k8_0 + (hc - b * n8);
-        const int rel = k8 - (kb0 << 2);  // half-slot inside the split's range
-        if (h < nhs && rel >= 0 && rel < (nkbs << 2)) {
+        const int k8i = (tid >> 3) + n * (kBgThreads / kBgMaxBatch);
+        const int rel = k8_0 + k8i - (kb0 << 2);  // 8-k group inside the split's range
+        if (seq_live && k8i < n8 && rel >= 0 && rel < (nkbs << 2)) {
             float y[8] = {xa[n][0].x, xa[n][0].y, xa[n][0].z, xa[n][0].w,
                           xa[n][1].x, xa[n][1].y, xa[n][1].z, xa[n][1].w};
             if constexpr (NORM) {
-                const float iv = inv[b];
+                const float iv = inv[sb];
                 const float wv[8] = {xw[n][0].x, xw[n][0].y, xw[n][0].z, xw[n][0].w,
                                      xw[n][1].x, xw[n][1].y, xw[n][1].z, xw[n][1].w};
 #pragma unroll
@@ -263,12 +270,17 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
             u32x4 hi, lo;
             bg_split8(y, hi, lo);
             const int ib = rel >> 2, q = rel & 3;
-            img[ib * 64 + q * 16 + b] = hi;
-            img[ib * 64 + q * 16 + 8 + b] = lo;
+            img[ib * 64 + q * 16 + sb] = hi;
+            img[ib * 64 + q * 16 + 8 + sb] = lo;
         }
     }
     __syncthreads();
 
+    const unsigned long long t_staged = in.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+#ifdef BG_LATE_W
+    load_step(0, wa);
+    load_step(1, wb);
+#endif
     // ---- 5. stream the tiles
     bg_float4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
     const u32x4* wimg = img + (size_t)(wb0 - kb0) * 64 + lane;
@@ -312,6 +324,12 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
     if (k < nsteps) consume(k, wa);
     if (k + 1 < nsteps) consume(k + 1, wb);
     __syncthreads();
+    if (in.stamps && tid == 0) {
+        unsigned long long* p = in.stamps + (size_t)blockIdx.x * 4;
+        p[0] = t_entry;
+        p[1] = t_staged;
+        p[2] = __builtin_amdgcn_s_memrealtime();
+    }
 
     // ---- 6. epilogue (one split) or publish + the group's last arriver merges in split order
     const int items = ntg * 64;  // (tile, row pair i < 8, sequence slot b < 8)
@@ -350,6 +368,7 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
         }
     }
     epi.finish(keys, g, B);
+    if (in.stamps && tid == 0) in.stamps[(size_t)blockIdx.x * 4 + 3] = __builtin_amdgcn_s_memrealtime();
 }
 
 // ---------------------------------------------------------------- epilogues

@@ -616,7 +616,7 @@ int sli_model_create(const sli_model_config* cfg, const void* comm_id, sli_model
         SLI_CHECK(c.w_dtype == SLI_DT_F16, SLI_ERR_ARG, "batch > 1 needs fp16 weights (MFMA projections)");
         SLI_CHECK(c.dim % 32 == 0 && (c.ffn / c.tp_size) % 32 == 0 && ((c.n_heads / c.tp_size) * c.head_dim) % 32 == 0,
                   SLI_ERR_SHAPE, "batch > 1: projection inputs must be multiples of 32");
-        SLI_CHECK((size_t)B * c.dim <= (size_t)kBgMaxStageElems, SLI_ERR_SHAPE, "batch * dim too large to stage");
+        SLI_CHECK(c.dim <= kBgMaxStageK, SLI_ERR_SHAPE, "batch > 1: dim must be at most 4096 (RMS staging)");
     }
 
     SLI_HIP(hipSetDevice(c.device));
