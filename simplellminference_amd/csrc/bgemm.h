@@ -197,15 +197,6 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
     auto load_step = [&](int k, u32x4(&w)[kBgU]) {
         const int kk = min(k, nsteps - 1);
         const int j = kk / cpt, c = kk - j * cpt;
-#ifdef BG_CONTIG  // timing experiment only (wrong math): the same bytes as lane-contiguous 1 KiB pieces
-        const char* tb = reinterpret_cast<const char*>(W) + (size_t)(t0 + j) * 16 * row_bytes +
-                         (size_t)wave * (16 * row_bytes / kBgWaves);
-#pragma unroll
-        for (int u = 0; u < kBgU; ++u) {
-            const int pc = min(c * kBgU + u, max(wnb - 1, 0));
-            w[u] = load16<true>(tb + ((size_t)pc * 64 + lane) * 16);
-        }
-#else
         const int row = epi.row(t0 + j, lane & 15);
         const char* base = reinterpret_cast<const char*>(W) + (size_t)row * row_bytes + (size_t)q8 * 2;
 #pragma unroll
@@ -213,14 +204,11 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
             const int bi = wb0 + min(c * kBgU + u, max(wnb - 1, 0));
             w[u] = load16<true>(base + (size_t)bi * 64);
         }
-#endif
     };
     u32x4 wa[kBgU], wb[kBgU];
-#ifndef BG_LATE_W
     load_step(0, wa);
     load_step(1, wb);
     __builtin_amdgcn_sched_barrier(0);
-#endif
 
     // ---- 3. per-sequence RMS over the full K (rms_kernel.cpp:12-19)
     if constexpr (NORM) {
@@ -277,10 +265,6 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
     __syncthreads();
 
     const unsigned long long t_staged = in.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
-#ifdef BG_LATE_W
-    load_step(0, wa);
-    load_step(1, wb);
-#endif
     // ---- 5. stream the tiles
     bg_float4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
     const u32x4* wimg = img + (size_t)(wb0 - kb0) * 64 + lane;
