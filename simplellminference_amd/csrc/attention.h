@@ -33,6 +33,7 @@ struct AttnArgs {
     float scale;            // 1/sqrt(hd) (mha_kernel.cpp:41)
     int seq_heads;          // kv heads per sequence: a batch is B sequences of seq_heads kv heads each
     int pos_seq_stride;     // int32s between consecutive sequences' positions at pos_dev
+    unsigned long long* stamps = nullptr;  // diagnostic (tools/attn_lab): per-workgroup s_memrealtime x4
 };
 
 // Position of the sequence that owns (batched) kv head kvh.
@@ -44,8 +45,8 @@ __device__ __forceinline__ int attn_pos(const AttnArgs<KT>& a, int kvh) {
 // A workgroup covers kAttnSlots wave-instructions of K (and of V) per lane-row group: WAVES waves of
 // NIT = kAttnSlots / WAVES vectors each. The split geometry (positions per workgroup) is therefore the
 // same for every WAVES; WAVES trades registers for latency hiding: 16 waves of 4 (MHA, GQA-2: each
-// wave starts computing as soon as its own few rows land, 4 waves per SIMD overlap) or 4 waves of 16
-// (GQA-4/8, whose G query heads need the register room of one wave per SIMD).
+// wave starts computing as soon as its own few rows land, 4 waves per SIMD overlap), 8 waves of 8
+// (GQA-4) or 4 waves of 16 (GQA-8, whose G query heads need the register room of one wave per SIMD).
 constexpr int kAttnSlots = 64;
 constexpr int kAttnMaxWgSplits = 128;  // combine-kernel capacity
 
@@ -58,17 +59,20 @@ struct AttnGeom {
     static_assert(LPR >= 1 && LPR <= 64 && (64 % LPR) == 0, "head_dim / vector shape");
 };
 
-__host__ __device__ constexpr int attn_waves(int g) { return g <= 2 ? 16 : 4; }
+// tools/attn_lab (profiles/r03_attn_lab.txt): MHA / GQA-2 16 waves, GQA-4 8, GQA-8 4; V loaded after the
+// scores (K and V never live together) up to GQA-4.
+__host__ __device__ constexpr int attn_waves(int g) { return g <= 2 ? 16 : g == 4 ? 8 : 4; }
+__host__ __device__ constexpr bool attn_late_v(int g) { return g <= 4; }
 
 // grid: n_kv_heads * wg_splits workgroups; wave w of workgroup (kvh, s) owns the w-th slice of split s.
 // The WAVES slice states are merged in LDS, so one partial per (q head, workgroup) reaches the workspace.
 // The split work of workgroup (kvh, wgs): partial state published write-through, arrival counted.
 // Returns true in the head's last-arriving workgroup (which must then merge the head: attn_merge).
 // Every return is uniform over the workgroup.
-template <typename KT, int HD, int G>
+template <typename KT, int HD, int G, int WAVES = attn_waves(G), bool LATE_V = attn_late_v(G)>
 __device__ __forceinline__ bool attn_publish(const AttnArgs<KT>& a, int kvh, int wgs) {
     using Geo = AttnGeom<KT, HD>;
-    constexpr int WAVES = attn_waves(G), kAttnNit = kAttnSlots / WAVES;
+    constexpr int kAttnNit = kAttnSlots / WAVES;
     constexpr int EPV = Geo::EPV, LPR = Geo::LPR, RPI = Geo::RPI, PPW = kAttnNit * RPI;
     __shared__ float sh[WAVES][G][HD + 2];
     __shared__ int last;
@@ -99,11 +103,16 @@ __device__ __forceinline__ bool attn_publish(const AttnArgs<KT>& a, int kvh, int
             const int t = min(t0 + it * RPI + sub, t_end - 1);  // clamp, never branch around a load
             kr[it] = load16<false>(kb + (long long)t * a.pos_stride);
         }
+        auto load_v = [&]() {
 #pragma unroll
-        for (int it = 0; it < kAttnNit; ++it) {
-            const int t = min(t0 + it * RPI + sub, t_end - 1);
-            vr[it] = load16<false>(vb + (long long)t * a.pos_stride);
-        }
+            for (int it = 0; it < kAttnNit; ++it) {
+                const int t = min(t0 + it * RPI + sub, t_end - 1);
+                vr[it] = load16<false>(vb + (long long)t * a.pos_stride);
+            }
+        };
+        // LATE_V: V is loaded once the scores are done, so K and V never occupy registers together
+        // (GQA-4/8 carry G query heads per lane: fewer registers = more resident workgroups)
+        if constexpr (!LATE_V) load_v();
         float qv[G][EPV];
 #pragma unroll
         for (int g = 0; g < G; ++g)
@@ -125,6 +134,7 @@ __device__ __forceinline__ bool attn_publish(const AttnArgs<KT>& a, int kvh, int
                 m[g] = fmaxf(m[g], s[it][g]);
             }
         }
+        if constexpr (LATE_V) load_v();
 #pragma unroll
         for (int g = 0; g < G; ++g)
 #pragma unroll
@@ -152,6 +162,7 @@ __device__ __forceinline__ bool attn_publish(const AttnArgs<KT>& a, int kvh, int
             }
         }
     }
+    if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 4 + 1] = __builtin_amdgcn_s_memrealtime();
     if (sub == 0) {
 #pragma unroll
         for (int g = 0; g < G; ++g) {
@@ -196,6 +207,7 @@ __device__ __forceinline__ bool attn_publish(const AttnArgs<KT>& a, int kvh, int
         if (last) __hip_atomic_store(a.counters + kvh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
+    if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 4 + 2] = __builtin_amdgcn_s_memrealtime();
     return last != 0;
 }
 
@@ -266,12 +278,15 @@ __device__ __forceinline__ int attn_live_splits(const AttnArgs<KT>& a, int kvh) 
     return min(attn_pos(a, kvh) / PPWG + 1, a.max_splits);
 }
 
-// grid: n_kv_heads * wg_splits workgroups of 64 * attn_waves(G) threads
-template <typename KT, int HD, int G>
-__global__ void __launch_bounds__(64 * attn_waves(G)) attn_partial_kernel(AttnArgs<KT> a) {
+// grid: n_kv_heads * wg_splits workgroups of 64 * WAVES threads
+template <typename KT, int HD, int G, int WAVES = attn_waves(G), bool LATE_V = attn_late_v(G)>
+__global__ void __launch_bounds__(64 * WAVES) attn_partial_kernel(AttnArgs<KT> a) {
+    if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 4] = __builtin_amdgcn_s_memrealtime();
     const int kvh = blockIdx.x / a.max_splits;  // max_splits counts workgroup splits here
-    if (attn_publish<KT, HD, G>(a, kvh, blockIdx.x - kvh * a.max_splits))
+    if (attn_publish<KT, HD, G, WAVES, LATE_V>(a, kvh, blockIdx.x - kvh * a.max_splits)) {
         attn_merge<HD, G>(a.part, a.out, kvh, a.max_splits, attn_live_splits<KT, HD, G>(a, kvh), 0, blockDim.x);
+        if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 4 + 3] = __builtin_amdgcn_s_memrealtime();
+    }
 }
 
 }  // namespace sli
