@@ -148,3 +148,20 @@ def test_llama3_8b_full_batch8_properties(gpu):
     wb, kb = gm.step_bytes()
     assert abs(wb - 15.009e9) / 15.009e9 < 0.01 and abs(kb - 4.295e9) / 4.295e9 < 0.01
     gm.close()
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_batch_tp_shard_step_nocomm(gpu, monkeypatch, world):
+    """One rank of a C4-shaped tensor-parallel batch (Llama-3-8B shapes, 2 layers, batch 8): the rank's
+    shard geometry (1 kv head per rank at TP 8, FFN 1792, vocab shard 16032) plans, allocates and steps
+    without a communicator (SLI_DEBUG_NOCOMM: placement and kernel shapes only; values are not a model)."""
+    from simplellminference_amd.model import LlamaModel, preset
+    monkeypatch.setenv("SLI_DEBUG_NOCOMM", "1")
+    cfg = preset("llama3-8b", num_hidden_layers=2)
+    m = LlamaModel(config=cfg, w_dtype="f16", kv_dtype="f16", seed=1, batch=8, tp_rank=world - 1,
+                   tp_size=world).init()
+    m.fill_kv_synthetic(7, 4095)
+    a = m.forward_batch([5 + b for b in range(8)], [4095, 17, 4000, 1, 2048, 3000, 4095, 9])
+    b = m.forward_batch([5 + b for b in range(8)], [4095, 17, 4000, 1, 2048, 3000, 4095, 9])
+    assert a.shape == (8, m.local_vocab) and np.isfinite(a).all() and np.array_equal(a, b)
+    m.close()
