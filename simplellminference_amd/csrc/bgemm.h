@@ -176,19 +176,18 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
     const int sb = tid & (kBgMaxBatch - 1);
     const bool seq_live = sb < B;
     const int sbc = min(sb, B - 1);
-    float4 xa[kBgNH][2], xw[kBgNH][2];
+    float4 xa[kBgNH][2];
 #pragma unroll
     for (int n = 0; n < kBgNH; ++n) {
         const int k8 = k8_0 + min((tid >> 3) + n * (kBgThreads / kBgMaxBatch), n8 - 1);  // clamp, never branch
         const float4* xp = reinterpret_cast<const float4*>(in.x + (size_t)sbc * K + (size_t)k8 * 8);
         xa[n][0] = xp[0];
         xa[n][1] = xp[1];
-        if constexpr (NORM) {
-            const float4* wp = reinterpret_cast<const float4*>(in.norm_w + (size_t)k8 * 8);
-            xw[n][0] = wp[0];
-            xw[n][1] = wp[1];
-        }
     }
+    // the norm weight once per workgroup (one float4 per thread, K <= 4096), shared through LDS: the
+    // per-sequence copies would double the staging loads, the slow part of the prologue
+    float4 wn{};
+    if constexpr (NORM) wn = reinterpret_cast<const float4*>(in.norm_w)[min(tid, (K >> 2) - 1)];
     __builtin_amdgcn_sched_barrier(0);
 
     // ---- 2. the first two weight steps
@@ -212,6 +211,7 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
 
     // ---- 3. per-sequence RMS over the full K (rms_kernel.cpp:12-19)
     if constexpr (NORM) {
+        if (tid < (K >> 2)) reinterpret_cast<float4*>(P)[tid] = wn;  // P is free until the stream
         float ss = 0.0f;
 #pragma unroll
         for (int n = 0; n < kBgNH; ++n) {
@@ -250,8 +250,9 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
                           xa[n][1].x, xa[n][1].y, xa[n][1].z, xa[n][1].w};
             if constexpr (NORM) {
                 const float iv = inv[sb];
-                const float wv[8] = {xw[n][0].x, xw[n][0].y, xw[n][0].z, xw[n][0].w,
-                                     xw[n][1].x, xw[n][1].y, xw[n][1].z, xw[n][1].w};
+                const float4 w0 = reinterpret_cast<const float4*>(P)[2 * (k8_0 + k8i)];
+                const float4 w1 = reinterpret_cast<const float4*>(P)[2 * (k8_0 + k8i) + 1];
+                const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
                 for (int e = 0; e < 8; ++e) y[e] = (y[e] * iv) * wv[e];  // rms_kernel.cpp:20-22
             }
