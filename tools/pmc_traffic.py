@@ -17,9 +17,13 @@ for r in csv.DictReader(open(path)):
     if r.get("Counter_Name") != "FETCH_SIZE":
         continue
     per[r["Kernel_Name"]].append(float(r["Counter_Value"]))
-gemv = [v for k, vs in per.items() if "gemv_kernel" in k for v in vs]
+def weight_kernel(k):  # the step's weight-streaming kernels: batch-1 GEMV or the batched MFMA projection
+    return "gemv_kernel" in k or "bgemm_kernel" in k
+
+
+gemv = [v for k, vs in per.items() if weight_kernel(k) for v in vs]
 if not gemv:
-    raise SystemExit("no gemv_kernel dispatches with FETCH_SIZE in " + path)
+    raise SystemExit("no gemv_kernel / bgemm_kernel dispatches with FETCH_SIZE in " + path)
 kb = sum(gemv) / len(gemv)
 res = {}
 try:
@@ -29,10 +33,13 @@ except (OSError, ValueError):
 res[key] = {
     "hbm_bytes_per_launch": round(2 * kb * 1024),
     "fetch_size_kib_per_launch_raw": round(kb, 1),
-    "correction": "x2: gfx950 FETCH_SIZE counts half the bytes of a coalesced 16-B/lane stream",
+    "correction": ("x2: gfx950 FETCH_SIZE counts half the bytes of a coalesced 16-B/lane stream"
+                   + ("" if "bgemm" not in "".join(per) else "; bgemm's 16-row x 64-B fragment loads are "
+                      "not calibrated against that rule")),
     "algorithmic_bytes_per_launch": round(alg),
     "gemv_dispatches": len(gemv),
-    "per_kernel_mean_kib_raw": {k.split("(")[0][:90]: round(sum(v) / len(v), 1) for k, v in per.items() if "gemv" in k},
+    "per_kernel_mean_kib_raw": {k.split("(")[0][:90]: round(sum(v) / len(v), 1) for k, v in per.items()
+                                if weight_kernel(k)},
 }
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res[key], indent=1))
