@@ -317,6 +317,16 @@ __global__ void get_kv_kernel(const KT* __restrict__ cache, float* out, int hkv,
 }
 
 // ---------------------------------------------------------------- the step
+// Vectors in flight per lane: the per-shape U (fp16, tools/gemv_lab) halved for int8, whose 16-byte
+// vector holds twice the columns: the same columns per chunk, two chunks per 4096-column row instead of
+// one, so a wave's second buffer streams while the first is consumed (measured C3: 414 -> 447 tok/s;
+// a quarter U: 431).
+template <typename WT, int R, int U, bool NT, class Epi>
+static hipError_t launch_gemv_u(const WT* W, const GemvIn& in, const Epi& epi, int units, hipStream_t s) {
+    constexpr int UW = std::is_same<WT, int8_t>::value && U >= 2 ? U / 2 : U;
+    return launch_gemv<WT, R, UW, NT>(W, in, epi, units, s);
+}
+
 template <typename WT, typename KT>
 struct StepRecorder {
     static constexpr bool NT = true;  // streamed-once weights: non-temporal loads
@@ -326,7 +336,7 @@ struct StepRecorder {
         KT* kc = (KT*)m->kc + (size_t)l * m->hkv * m->T * m->hd;
         KT* vc = (KT*)m->vc + (size_t)l * m->hkv * m->T * m->hd;
         EpiQKV<KT> e{m->q, kc, vc, w.qkv_s, &m->st->pos, m->sin_t, m->cos_t, m->hq, m->hkv, m->hd, m->T};
-        SLI_HIP((launch_gemv<WT, 2, 4, NT>((const WT*)w.qkv, in, e, (m->hq + 2 * m->hkv) * (m->hd / 2), m->stream)));
+        SLI_HIP((launch_gemv_u<WT, 2, 4, NT>((const WT*)w.qkv, in, e, (m->hq + 2 * m->hkv) * (m->hd / 2), m->stream)));
         return SLI_OK;
     }
     static int gemv_wo(sli_model* m, int l) {
@@ -334,14 +344,14 @@ struct StepRecorder {
         const bool tp = m->partial;
         GemvIn in{m->attn, nullptr, 0.0f, m->hq * m->hd};
         EpiStore<1> e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, w.wo_s, 1.0f, m->D};
-        SLI_HIP((launch_gemv<WT, 1, 2, NT>((const WT*)w.wo, in, e, m->D, m->stream)));
+        SLI_HIP((launch_gemv_u<WT, 1, 2, NT>((const WT*)w.wo, in, e, m->D, m->stream)));
         return SLI_OK;
     }
     static int gemv_gu(sli_model* m, int l) {
         const LayerW& w = m->layers[l];
         GemvIn in{m->x, m->norms + (size_t)(2 * l + 1) * m->D, m->c.eps, m->D};
         EpiSwiGLU e{m->act, w.gu_s, m->Il, m->c.act_mode};
-        SLI_HIP((launch_gemv<WT, 2, 4, NT>((const WT*)w.gu, in, e, m->Il, m->stream)));
+        SLI_HIP((launch_gemv_u<WT, 2, 4, NT>((const WT*)w.gu, in, e, m->Il, m->stream)));
         return SLI_OK;
     }
     static int gemv_down(sli_model* m, int l) {
@@ -349,7 +359,7 @@ struct StepRecorder {
         const bool tp = m->partial;
         GemvIn in{m->act, nullptr, 0.0f, m->Il};
         EpiStore<1> e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, w.down_s, 1.0f, m->D};
-        SLI_HIP((launch_gemv<WT, 1, 6, NT>((const WT*)w.down, in, e, m->D, m->stream)));
+        SLI_HIP((launch_gemv_u<WT, 1, 6, NT>((const WT*)w.down, in, e, m->D, m->stream)));
         return SLI_OK;
     }
     static int lm_head_blocks(sli_model* m) { return gemv_blocks((m->v_n + 1) / 2); }
@@ -357,7 +367,7 @@ struct StepRecorder {
         GemvIn in{m->x, m->norms + (size_t)(2 * m->L) * m->D, m->c.eps, m->D};
         EpiLogits<2> e{m->logits, m->keys, m->emb_s ? m->emb_s + m->v_lo : nullptr, m->v_n, m->v_lo, 0ull};
         const WT* w = (const WT*)m->emb + (size_t)m->v_lo * m->D;
-        SLI_HIP((launch_gemv<WT, 2, 4, NT>(w, in, e, (m->v_n + 1) / 2, m->stream)));
+        SLI_HIP((launch_gemv_u<WT, 2, 4, NT>(w, in, e, (m->v_n + 1) / 2, m->stream)));
         return SLI_OK;
     }
     static int allreduce_x(sli_model* m) {
