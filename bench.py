@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample budget")
     ap.add_argument("--gemv-iters", type=int, default=20)
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r03_gemv_traffic.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r04_gemv_traffic.json"))
     return ap.parse_args()
 
 

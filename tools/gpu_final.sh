@@ -4,7 +4,7 @@
 #   tools/gpu_final.sh <tag>
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-tag=${1:-r03}
+tag=${1:-r04}
 mkdir -p gpurun_out
 KEY=llama2-7b/f16/tp1 ./tools/pmc_traffic.sh $tag || exit 1
 KEY=llama2-7b/i8/tp1 ./tools/pmc_traffic.sh $tag --w-dtype i8 || exit 1
@@ -12,6 +12,10 @@ KEY=llama3-8b/f16/tp1/b8 ./tools/pmc_traffic.sh $tag --preset llama3-8b --ctx 40
 cp gpurun_out/pmc/${tag}_gemv_traffic.json profiles/${tag}_gemv_traffic.json
 ./tools/gpu_round.sh $tag || exit 1
 ./tools/prof_step.sh ${tag}_c1 || exit 1
-python3 tools/step_trace.py $(find gpurun_out/prof -name "${tag}_c1_kernel_trace.csv" | head -1) > gpurun_out/prof/${tag}_c1_step_trace.txt
-cat gpurun_out/prof/${tag}_c1_step_trace.txt
+./tools/prof_step.sh ${tag}_c3 --w-dtype i8 || exit 1
+./tools/prof_step.sh ${tag}_c4 --preset llama3-8b --ctx 4096 --batch 8 || exit 1
+for c in c1 c3 c4; do
+  python3 tools/step_trace.py $(find gpurun_out/prof -name "${tag}_${c}_kernel_trace.csv" | head -1) > gpurun_out/prof/${tag}_${c}_step_trace.txt
+  tail -1 gpurun_out/prof/${tag}_${c}_step_trace.txt
+done
 echo final done
