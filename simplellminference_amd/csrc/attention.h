@@ -179,7 +179,7 @@ __device__ __forceinline__ bool attn_publish(const AttnArgs<KT>& a, int kvh, int
     // head's last-arriving workgroup can read it from any XCD without a fence pair
     // (MI355X_MICROARCH.md, hand-off table row 1: sc1 stores, drained, one agent-scope add per
     // workgroup behind a workgroup barrier, sc1 loads by the last adder after the barrier it joins).
-    for (int i = threadIdx.x; i < G * HD; i += blockDim.x) {
+    for (int i = threadIdx.x; i < G * HD; i += 64 * WAVES) {
         const int g = i / HD, d = i - g * HD;
         float M = -INFINITY;
 #pragma unroll
@@ -284,7 +284,7 @@ __global__ void __launch_bounds__(64 * WAVES) attn_partial_kernel(AttnArgs<KT> a
     if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 4] = __builtin_amdgcn_s_memrealtime();
     const int kvh = blockIdx.x / a.max_splits;  // max_splits counts workgroup splits here
     if (attn_publish<KT, HD, G, WAVES, LATE_V>(a, kvh, blockIdx.x - kvh * a.max_splits)) {
-        attn_merge<HD, G>(a.part, a.out, kvh, a.max_splits, attn_live_splits<KT, HD, G>(a, kvh), 0, blockDim.x);
+        attn_merge<HD, G>(a.part, a.out, kvh, a.max_splits, attn_live_splits<KT, HD, G>(a, kvh), 0, 64 * WAVES);
         if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 4 + 3] = __builtin_amdgcn_s_memrealtime();
     }
 }

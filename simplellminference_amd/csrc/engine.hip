@@ -232,16 +232,23 @@ static float synth_c(const sli_model* m, int kind) {
 }
 
 // ---------------------------------------------------------------- small kernels of the step
-__global__ void keyreduce_kernel(const unsigned long long* __restrict__ keys, int n, DevState* st) {
+// Second argmax stage (256 threads). FINALIZE: the step has no cross-rank key exchange, so the same
+// thread that reduced the key also advances the state (one launch instead of keyreduce + finalize).
+constexpr int kKeyThreads = 256;
+template <bool FINALIZE>
+__global__ void __launch_bounds__(kKeyThreads) keyreduce_kernel(const unsigned long long* __restrict__ keys, int n,
+                                                                DevState* st, const int32_t* __restrict__ prompt,
+                                                                int32_t* hist, int T) {
     unsigned long long b = 0;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) b = keys[i] > b ? keys[i] : b;
+    for (int i = threadIdx.x; i < n; i += kKeyThreads) b = keys[i] > b ? keys[i] : b;
     b = wave_max_u64(b);
-    __shared__ unsigned long long red[4];
+    __shared__ unsigned long long red[kKeyThreads / 64];
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = b;
     __syncthreads();
     if (threadIdx.x == 0) {
-        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) b = red[w] > b ? red[w] : b;
+        for (int w = 1; w < kKeyThreads / 64; ++w) b = red[w] > b ? red[w] : b;
         st->key = red[0] > b ? red[0] : b;
+        if constexpr (FINALIZE) finalize_state(st, prompt, hist, T);
     }
 }
 
@@ -485,9 +492,16 @@ struct StepRecorder {
             SLI_TRY(allreduce_x(m));
         }
         SLI_TRY(gemv_lm(m));
-        hipLaunchKernelGGL(keyreduce_kernel, dim3(1), dim3(256), 0, s, m->keys, lm_head_blocks(m), m->st);
+        if (!m->collectives) {
+            hipLaunchKernelGGL(keyreduce_kernel<true>, dim3(1), dim3(kKeyThreads), 0, s, m->keys, lm_head_blocks(m),
+                               m->st, m->prompt, m->hist, m->T);
+            SLI_HIP(hipGetLastError());
+            return SLI_OK;
+        }
+        hipLaunchKernelGGL(keyreduce_kernel<false>, dim3(1), dim3(kKeyThreads), 0, s, m->keys, lm_head_blocks(m), m->st,
+                           m->prompt, m->hist, m->T);
         SLI_HIP(hipGetLastError());
-        if (m->collectives) SLI_NCCL(ncclAllReduce(&m->st->key, &m->st->key, 1, ncclUint64, ncclMax, m->comm, s));
+        SLI_NCCL(ncclAllReduce(&m->st->key, &m->st->key, 1, ncclUint64, ncclMax, m->comm, s));
         hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1), 0, s, m->st, m->prompt, m->hist, m->T);
         SLI_HIP(hipGetLastError());
         return SLI_OK;

@@ -52,7 +52,7 @@ struct XStage {
     float4 xr[kGemvStageV4];
     float4 wr[kGemvStageV4];
     __device__ __forceinline__ void issue(const GemvIn& in) {
-        const int tid = threadIdx.x, nt = blockDim.x, n4 = in.cols >> 2;
+        const int tid = threadIdx.x, nt = kGemvThreads, n4 = in.cols >> 2;
         const float4* x4 = reinterpret_cast<const float4*>(in.x);
         // unconditional (clamped) loads: a load under a branch would make the weight waits conservative
         const float4* w4 = reinterpret_cast<const float4*>(in.norm_w ? in.norm_w : in.x);
@@ -67,7 +67,7 @@ struct XStage {
     __device__ __forceinline__ void commit(float* smem, const GemvIn& in) {
         float* red = smem;
         float4* xs4 = reinterpret_cast<float4*>(smem + kGemvLdsHead);
-        const int tid = threadIdx.x, nt = blockDim.x, n4 = in.cols >> 2;
+        const int tid = threadIdx.x, nt = kGemvThreads, n4 = in.cols >> 2;
         if (in.norm_w == nullptr) {
 #pragma unroll
             for (int k = 0; k < kGemvStageV4; ++k) xs4[xswz<G>(min(tid + k * nt, n4 - 1))] = xr[k];
@@ -181,7 +181,7 @@ __device__ __forceinline__ void gemv_block(const WT* __restrict__ W, const GemvI
     constexpr int CV = U * 64;  // vectors per row per chunk
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nwaves = blockDim.x >> 6;
+    const int nwaves = kGemvThreads >> 6;  // compile-time: blockDim.x is a dispatch-packet load
     const int nvec = in.cols / EPV;
     const size_t row_bytes = (size_t)in.cols * sizeof(WT);
     const int nunits = epi.units();
@@ -198,6 +198,10 @@ __device__ __forceinline__ void gemv_block(const WT* __restrict__ W, const GemvI
     const unsigned long long t_entry = in.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
     unsigned long long t_staged = 0;
     stage.issue(in);
+    // the epilogue's own inputs for this thread's unit (the store loop's first unit): in flight with the
+    // input, landed long before the stream ends instead of a round trip after it
+    const int pre_unit = max(min(ub + (int)threadIdx.x, nunits - 1), 0);
+    epi.prefetch_a(pre_unit);
     __builtin_amdgcn_sched_barrier(0);  // keep every input load ahead of the weight loads
 
     // (u, c) = unit and chunk of a step; the load position saturates at the wave's last step
@@ -253,6 +257,7 @@ __device__ __forceinline__ void gemv_block(const WT* __restrict__ W, const GemvI
     __builtin_amdgcn_sched_barrier(0);
     stage.commit(smem, in);
     __syncthreads();
+    epi.prefetch_b(pre_unit);
     t_staged = in.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
     int k = 0;
     for (; k + 2 < nsteps; k += 2) {
@@ -271,7 +276,7 @@ __device__ __forceinline__ void gemv_block(const WT* __restrict__ W, const GemvI
         if (k + 1 < nsteps) consume_step(cu, cc, wb);
     }
     __syncthreads();
-    for (int u = ub + (int)threadIdx.x; u < ue; u += blockDim.x) {
+    for (int u = ub + (int)threadIdx.x; u < ue; u += kGemvThreads) {
         int rows[R];
         epi.rows(u, rows);
         epi.store(u, rows, res + (u - ub) * R);
@@ -324,19 +329,36 @@ struct EpiStore {
     const float* rscale;
     float scale;
     int nrows;
+    int pre_u = -1;  // unit whose residual / row scales were prefetched at kernel entry
+    float pre_r[R] = {}, pre_s[R] = {};
     __device__ int units() const { return (nrows + R - 1) / R; }
     __device__ void rows(int u, int* r) const {
 #pragma unroll
         for (int i = 0; i < R; ++i) r[i] = min(u * R + i, nrows - 1);
     }
+    // Entry prefetch (issued before the weight stream, consumed after it): unconditional loads from
+    // selected valid pointers, so no branch makes the compiler's vmcnt waits conservative.
+    __device__ void prefetch_a(int u) {
+        pre_u = u;
+        const float* rp = resid ? resid : y;
+        const float* sp = rscale ? rscale : y;
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const int row = min(u * R + i, nrows - 1);
+            pre_r[i] = rp[row];
+            pre_s[i] = sp[row];
+        }
+    }
+    __device__ void prefetch_b(int) {}
     __device__ void store(int u, const int*, const float* v) const {
+        const bool pre = u == pre_u;
 #pragma unroll
         for (int i = 0; i < R; ++i) {
             const int row = u * R + i;
             if (row < nrows) {
-                float a = rscale ? v[i] * rscale[row] : v[i];
+                float a = rscale ? v[i] * (pre ? pre_s[i] : rscale[row]) : v[i];
                 a = a * scale;
-                y[row] = resid ? resid[row] + a : a;
+                y[row] = resid ? (pre ? pre_r[i] : resid[row]) + a : a;
             }
         }
     }
@@ -357,7 +379,25 @@ struct EpiQKV {
     const float* sin_t;        // [T][hd/2]
     const float* cos_t;
     int hq, hkv, hd, T;
+    int pre_u = -1, pre_pos = 0;  // entry prefetch: position, row scales; then the RoPE table entries
+    float pre_s0 = 1.0f, pre_s1 = 1.0f, pre_sin = 0.0f, pre_cos = 1.0f;
     __device__ int units() const { return (hq + 2 * hkv) * (hd / 2); }
+    __device__ void prefetch_a(int u) {
+        pre_u = u;
+        pre_pos = *pos_dev;
+        int r[2];
+        rows(u, r);
+        const float* sp = rscale ? rscale : sin_t;
+        pre_s0 = sp[r[0]];
+        pre_s1 = sp[r[1]];
+    }
+    // after the input commit (the position has landed with the input): the table row of this position
+    __device__ void prefetch_b(int u) {
+        const int half = hd / 2;
+        const int d = u - (u / half) * half;
+        pre_sin = sin_t[pre_pos * half + d];
+        pre_cos = cos_t[pre_pos * half + d];
+    }
     __device__ void rows(int u, int* r) const {
         const int half = hd / 2;
         const int uh = u / half;
@@ -369,14 +409,15 @@ struct EpiQKV {
         const int half = hd / 2;
         const int uh = u / half;
         const int d = u - uh * half;
+        const bool pre = u == pre_u;
         float a0 = acc[0], a1 = acc[1];
         if (rscale) {
-            a0 *= rscale[r[0]];
-            a1 *= rscale[r[1]];
+            a0 *= pre ? pre_s0 : rscale[r[0]];
+            a1 *= pre ? pre_s1 : rscale[r[1]];
         }
-        const int pos = *pos_dev;
+        const int pos = pre ? pre_pos : *pos_dev;
         if (uh < hq + hkv) {  // q or k: rotate (rope_kernel.cpp:30-38)
-            const float fci = sin_t[pos * half + d], fcr = cos_t[pos * half + d];
+            const float fci = pre ? pre_sin : sin_t[pos * half + d], fcr = pre ? pre_cos : cos_t[pos * half + d];
             const float r0 = a0 * fcr - a1 * fci;
             const float r1 = a1 * fcr + a0 * fci;
             if (uh < hq) {
@@ -404,16 +445,26 @@ struct EpiSwiGLU {
     const float* rscale;
     int inter;  // I (local)
     int silu;
+    int pre_u = -1;
+    float pre_s0 = 1.0f, pre_s1 = 1.0f;
     __device__ int units() const { return inter; }
     __device__ void rows(int u, int* r) const {
         r[0] = u;
         r[1] = inter + u;
     }
+    __device__ void prefetch_a(int u) {
+        pre_u = u;
+        const float* sp = rscale ? rscale : act;
+        pre_s0 = sp[rscale ? u : 0];
+        pre_s1 = sp[rscale ? inter + u : 0];
+    }
+    __device__ void prefetch_b(int) {}
     __device__ void store(int u, const int* r, const float* acc) const {
+        const bool pre = u == pre_u;
         float g = acc[0], up = acc[1];
         if (rscale) {
-            g *= rscale[r[0]];
-            up *= rscale[r[1]];
+            g *= pre ? pre_s0 : rscale[r[0]];
+            up *= pre ? pre_s1 : rscale[r[1]];
         }
         float t = 1.0f / (1.0f + expf(-g));
         if (silu) t = g * t;
@@ -433,17 +484,27 @@ struct EpiLogits {
     int nrows;
     int vocab_off;
     unsigned long long best;
+    int pre_u = -1;
+    float pre_s[R] = {};
     __device__ int units() const { return (nrows + R - 1) / R; }
     __device__ void rows(int u, int* r) const {
 #pragma unroll
         for (int i = 0; i < R; ++i) r[i] = min(u * R + i, nrows - 1);
     }
+    __device__ void prefetch_a(int u) {
+        pre_u = u;
+        const float* sp = rscale ? rscale : logits;
+#pragma unroll
+        for (int i = 0; i < R; ++i) pre_s[i] = sp[min(u * R + i, nrows - 1)];
+    }
+    __device__ void prefetch_b(int) {}
     __device__ void store(int u, const int*, const float* acc) {
+        const bool pre = u == pre_u;
 #pragma unroll
         for (int i = 0; i < R; ++i) {
             const int row = u * R + i;
             if (row < nrows) {
-                const float a = rscale ? acc[i] * rscale[row] : acc[i];
+                const float a = rscale ? acc[i] * (pre ? pre_s[i] : rscale[row]) : acc[i];
                 logits[row] = a;
                 const unsigned long long k = argmax_key(a, (unsigned)(row + vocab_off));
                 best = k > best ? k : best;
@@ -459,7 +520,7 @@ struct EpiLogits {
         __syncthreads();
         if (threadIdx.x == 0) {
             unsigned long long b = 0;
-            for (int w = 0; w < (int)(blockDim.x >> 6); ++w) b = red[w] > b ? red[w] : b;
+            for (int w = 0; w < (kGemvThreads >> 6); ++w) b = red[w] > b ? red[w] : b;
             keys[blockIdx.x] = b;
         }
     }

@@ -9,7 +9,7 @@ mkdir -p gpurun_out
 KEY=llama2-7b/f16/tp1 ./tools/pmc_traffic.sh $tag || exit 1
 KEY=llama2-7b/i8/tp1 ./tools/pmc_traffic.sh $tag --w-dtype i8 || exit 1
 KEY=llama3-8b/f16/tp1/b8 ./tools/pmc_traffic.sh $tag --preset llama3-8b --ctx 4096 --batch 8 || exit 1
-cp gpurun_out/pmc/${tag}_gemv_traffic.json profiles/${tag}_gemv_traffic.json
+cp gpurun_out/pmc/${tag}_gemv_traffic.json profiles/${tag}_gemv_traffic.json || exit 1
 ./tools/gpu_round.sh $tag || exit 1
 ./tools/prof_step.sh ${tag}_c1 || exit 1
 ./tools/prof_step.sh ${tag}_c3 --w-dtype i8 || exit 1
