@@ -104,10 +104,12 @@ int main(int argc, char** argv) {
         const double gb = n * 2.0 / 1e9;
         BgPlan auto_p = bg_plan(tiles, sh.K, B, sh.norm);
         std::vector<BgPlan> cands = {auto_p};
+        const bool auto_only = getenv("LAB_AUTO_ONLY") != nullptr;
         const int tpws[] = {1, 2, 3, 4, 6, 8, 12, 16, 24, 32};
         const int sps[] = {1, 2, 4, 8};
         for (int sp : sps)
             for (int tpw : tpws) {
+                if (auto_only) break;
                 const int nkb = sh.K / 32;
                 if (sp > 1 && nkb / sp < kBgWaves) continue;
                 const int kbs = (nkb + sp - 1) / sp;
