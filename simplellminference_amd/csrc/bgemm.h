@@ -171,15 +171,28 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
     // ---- 1. activation staging loads, issued first (s_waitcnt vmcnt counts in issue order). Thread t
     // stages sequence b = t & 7 at the 8-k groups (t >> 3) + 128 n: the 8 lanes of a group write 8
     // consecutive 16-byte image slots (conflict-free ds_write_b128), the loads stay 32 B per lane.
+    // Without the fused RMS (wo, down) nothing needs the whole row, so every WAVE stages only its own
+    // blocks [wb0, wb0 + wnb) (the blocks its MFMAs read, for every tile of the workgroup) and starts
+    // streaming as soon as they land: no workgroup barrier behind the slowest wave's activations (the
+    // B*K*4-byte image is pulled through L2 by 256 workgroups at once; profiles/r04_bgemm_lab_*).
+    // Lane l: sequence l >> 3, block 2n + ((l >> 2) & 1), 8-k group l & 3: 8 lanes read 256
+    // contiguous bytes of one sequence row.
     const int n8 = NORM ? (K >> 3) : (nkbs << 2);  // 8-k groups per sequence in the staged range
     const int k8_0 = NORM ? 0 : (kb0 << 2);
-    const int sb = tid & (kBgMaxBatch - 1);
+    const int sb = NORM ? (tid & (kBgMaxBatch - 1)) : (lane >> 3);
     const bool seq_live = sb < B;
     const int sbc = min(sb, B - 1);
+    const int wq = lane & 3, wbo = (lane >> 2) & 1;  // per-wave staging: 8-k group, block offset
     float4 xa[kBgNH][2];
 #pragma unroll
     for (int n = 0; n < kBgNH; ++n) {
-        const int k8 = k8_0 + min((tid >> 3) + n * (kBgThreads / kBgMaxBatch), n8 - 1);  // clamp, never branch
+        int k8;
+        if constexpr (NORM) {
+            k8 = k8_0 + min((tid >> 3) + n * (kBgThreads / kBgMaxBatch), n8 - 1);  // clamp, never branch
+        } else {
+            const int blk = wb0 + max(min(2 * n + wbo, wnb - 1), 0);  // clamped into the row
+            k8 = min(blk, nkb - 1) * 4 + wq;
+        }
         const float4* xp = reinterpret_cast<const float4*>(in.x + (size_t)sbc * K + (size_t)k8 * 8);
         xa[n][0] = xp[0];
         xa[n][1] = xp[1];
@@ -241,8 +254,25 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
     }
 
     // ---- 4. the split's k-range of every sequence into LDS as B fragments (hi: column b, lo: 8 + b)
+    if constexpr (!NORM) {  // per wave: its own blocks, visible to its own later reads after lgkmcnt(0)
 #pragma unroll
-    for (int n = 0; n < kBgNH; ++n) {
+        for (int n = 0; n < kBgNH; ++n) {
+            const int bw = 2 * n + wbo;
+            if (seq_live && bw < wnb) {
+                const float y[8] = {xa[n][0].x, xa[n][0].y, xa[n][0].z, xa[n][0].w,
+                                    xa[n][1].x, xa[n][1].y, xa[n][1].z, xa[n][1].w};
+                u32x4 hi, lo;
+                bg_split8(y, hi, lo);
+                const int ib = wb0 - kb0 + bw;
+                img[ib * 64 + wq * 16 + sb] = hi;
+                img[ib * 64 + wq * 16 + 8 + sb] = lo;
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+    }
+#pragma unroll
+    for (int n = 0; NORM && n < kBgNH; ++n) {
         const int k8i = (tid >> 3) + n * (kBgThreads / kBgMaxBatch);
         const int rel = k8_0 + k8i - (kb0 << 2);  // 8-k group inside the split's range
         if (seq_live && k8i < n8 && rel >= 0 && rel < (nkbs << 2)) {
@@ -263,7 +293,7 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
             img[ib * 64 + q * 16 + 8 + sb] = lo;
         }
     }
-    __syncthreads();
+    if constexpr (NORM) __syncthreads();
 
     const unsigned long long t_staged = in.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
     // ---- 5. stream the tiles
