@@ -77,6 +77,7 @@ inline BgPlan bg_plan(int ntiles, int K, int B, bool norm, int cus = 256) {
     double best_cost = 1e30;
     for (int s = 1; s <= 16; ++s) {
         if (s > 1 && nkb / s < kBgWaves) break;  // every wave keeps at least one block per tile
+        if (norm && s > 1) break;  // the fused RMS needs the whole row in one workgroup (bgemm_kernel)
         const int kbs = (nkb + s - 1) / s;
         if (kbs * 32 > kBgMaxStageK) continue;  // staging registers
         for (int tpw = 1; tpw <= 64; ++tpw) {
@@ -177,30 +178,33 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
     // B*K*4-byte image is pulled through L2 by 256 workgroups at once; profiles/r04_bgemm_lab_*).
     // Lane l: sequence l >> 3, block 2n + ((l >> 2) & 1), 8-k group l & 3: 8 lanes read 256
     // contiguous bytes of one sequence row.
-    const int n8 = NORM ? (K >> 3) : (nkbs << 2);  // 8-k groups per sequence in the staged range
-    const int k8_0 = NORM ? 0 : (kb0 << 2);
-    const int sb = NORM ? (tid & (kBgMaxBatch - 1)) : (lane >> 3);
+    // With the fused RMS the norm is split the same way: the image holds x * w (rms_kernel.cpp:20-22
+    // without the per-sequence 1/rms), every wave adds its blocks' sum of squares to LDS, and the
+    // per-sequence 1/rms (:12-19) multiplies the finished row sums in the epilogue: a per-sequence scalar
+    // commutes with the k-sum. NORM plans have one split (bg_plan), so the waves' blocks cover the row.
+    const int sb = lane >> 3;
     const bool seq_live = sb < B;
     const int sbc = min(sb, B - 1);
     const int wq = lane & 3, wbo = (lane >> 2) & 1;  // per-wave staging: 8-k group, block offset
     float4 xa[kBgNH][2];
+    float4 wn[NORM ? kBgNH : 1][2];
 #pragma unroll
     for (int n = 0; n < kBgNH; ++n) {
-        int k8;
-        if constexpr (NORM) {
-            k8 = k8_0 + min((tid >> 3) + n * (kBgThreads / kBgMaxBatch), n8 - 1);  // clamp, never branch
-        } else {
-            const int blk = wb0 + max(min(2 * n + wbo, wnb - 1), 0);  // clamped into the row
-            k8 = min(blk, nkb - 1) * 4 + wq;
-        }
+        const int blk = wb0 + max(min(2 * n + wbo, wnb - 1), 0);  // clamped into the row, never a branch
+        const int k8 = min(blk, nkb - 1) * 4 + wq;
         const float4* xp = reinterpret_cast<const float4*>(in.x + (size_t)sbc * K + (size_t)k8 * 8);
         xa[n][0] = xp[0];
         xa[n][1] = xp[1];
     }
-    // the norm weight once per workgroup (one float4 per thread, K <= 4096), shared through LDS: the
-    // per-sequence copies would double the staging loads, the slow part of the prologue
-    float4 wn{};
-    if constexpr (NORM) wn = reinterpret_cast<const float4*>(in.norm_w)[min(tid, (K >> 2) - 1)];
+    if constexpr (NORM) {
+#pragma unroll
+        for (int n = 0; n < kBgNH; ++n) {
+            const int blk = wb0 + max(min(2 * n + wbo, wnb - 1), 0);
+            const float4* wp = reinterpret_cast<const float4*>(in.norm_w + (size_t)(min(blk, nkb - 1) * 4 + wq) * 8);
+            wn[n][0] = wp[0];
+            wn[n][1] = wp[1];
+        }
+    }
     __builtin_amdgcn_sched_barrier(0);
 
     // ---- 2. the first two weight steps
@@ -222,78 +226,39 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
     load_step(1, wb);
     __builtin_amdgcn_sched_barrier(0);
 
-    // ---- 3. per-sequence RMS over the full K (rms_kernel.cpp:12-19)
-    if constexpr (NORM) {
-        if (tid < (K >> 2)) reinterpret_cast<float4*>(P)[tid] = wn;  // P is free until the stream
-        float ss = 0.0f;
+    // ---- 3./4. this wave's blocks into LDS as B fragments (hi: column b, lo: 8 + b), visible to the
+    // wave's own later reads after lgkmcnt(0); NORM: x * w staged, this wave's sum of x^2 to red[wave][b]
+    float ss = 0.0f;
 #pragma unroll
-        for (int n = 0; n < kBgNH; ++n) {
+    for (int n = 0; n < kBgNH; ++n) {
+        const int bw = 2 * n + wbo;
+        float y[8] = {xa[n][0].x, xa[n][0].y, xa[n][0].z, xa[n][0].w, xa[n][1].x, xa[n][1].y, xa[n][1].z, xa[n][1].w};
+        if constexpr (NORM) {
             float v = 0.0f;
-            v += xa[n][0].x * xa[n][0].x;
-            v += xa[n][0].y * xa[n][0].y;
-            v += xa[n][0].z * xa[n][0].z;
-            v += xa[n][0].w * xa[n][0].w;
-            v += xa[n][1].x * xa[n][1].x;
-            v += xa[n][1].y * xa[n][1].y;
-            v += xa[n][1].z * xa[n][1].z;
-            v += xa[n][1].w * xa[n][1].w;
-            ss += ((tid >> 3) + n * (kBgThreads / kBgMaxBatch) < n8) ? v : 0.0f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v += y[e] * y[e];
+            ss += bw < wnb ? v : 0.0f;
+            const float wv[8] = {wn[n][0].x, wn[n][0].y, wn[n][0].z, wn[n][0].w,
+                                 wn[n][1].x, wn[n][1].y, wn[n][1].z, wn[n][1].w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) y[e] = y[e] * wv[e];
         }
-#pragma unroll
-        for (int o = 8; o < 64; o <<= 1) ss += __shfl_xor(ss, o, kWave);  // lanes of one sequence
-        if (lane < kBgMaxBatch) red[wave * 8 + lane] = ss;
-        __syncthreads();
-        if (tid < B) {
-            float t = 0.0f;
-            for (int w = 0; w < kBgWaves; ++w) t += red[w * 8 + tid];
-            const float tep = t / (float)K;         // rms_kernel.cpp:17
-            const float rms = sqrtf(tep + in.eps);  // :18
-            inv[tid] = 1.0f / rms;                  // :19
-        }
-        __syncthreads();
-    }
-
-    // ---- 4. the split's k-range of every sequence into LDS as B fragments (hi: column b, lo: 8 + b)
-    if constexpr (!NORM) {  // per wave: its own blocks, visible to its own later reads after lgkmcnt(0)
-#pragma unroll
-        for (int n = 0; n < kBgNH; ++n) {
-            const int bw = 2 * n + wbo;
-            if (seq_live && bw < wnb) {
-                const float y[8] = {xa[n][0].x, xa[n][0].y, xa[n][0].z, xa[n][0].w,
-                                    xa[n][1].x, xa[n][1].y, xa[n][1].z, xa[n][1].w};
-                u32x4 hi, lo;
-                bg_split8(y, hi, lo);
-                const int ib = wb0 - kb0 + bw;
-                img[ib * 64 + wq * 16 + sb] = hi;
-                img[ib * 64 + wq * 16 + 8 + sb] = lo;
-            }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
-    }
-#pragma unroll
-    for (int n = 0; NORM && n < kBgNH; ++n) {
-        const int k8i = (tid >> 3) + n * (kBgThreads / kBgMaxBatch);
-        const int rel = k8_0 + k8i - (kb0 << 2);  // 8-k group inside the split's range
-        if (seq_live && k8i < n8 && rel >= 0 && rel < (nkbs << 2)) {
-            float y[8] = {xa[n][0].x, xa[n][0].y, xa[n][0].z, xa[n][0].w,
-                          xa[n][1].x, xa[n][1].y, xa[n][1].z, xa[n][1].w};
-            if constexpr (NORM) {
-                const float iv = inv[sb];
-                const float4 w0 = reinterpret_cast<const float4*>(P)[2 * (k8_0 + k8i)];
-                const float4 w1 = reinterpret_cast<const float4*>(P)[2 * (k8_0 + k8i) + 1];
-                const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-#pragma unroll
-                for (int e = 0; e < 8; ++e) y[e] = (y[e] * iv) * wv[e];  // rms_kernel.cpp:20-22
-            }
+        if (seq_live && bw < wnb) {
             u32x4 hi, lo;
             bg_split8(y, hi, lo);
-            const int ib = rel >> 2, q = rel & 3;
-            img[ib * 64 + q * 16 + sb] = hi;
-            img[ib * 64 + q * 16 + 8 + sb] = lo;
+            const int ib = wb0 - kb0 + bw;
+            img[ib * 64 + wq * 16 + sb] = hi;
+            img[ib * 64 + wq * 16 + 8 + sb] = lo;
         }
     }
-    if constexpr (NORM) __syncthreads();
+    if constexpr (NORM) {
+        ss += __shfl_xor(ss, 1, kWave);  // the 8 lanes of one sequence
+        ss += __shfl_xor(ss, 2, kWave);
+        ss += __shfl_xor(ss, 4, kWave);
+        if ((lane & 7) == 0) red[wave * 8 + sb] = ss;  // read after the stream's final barrier
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
 
     const unsigned long long t_staged = in.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
     // ---- 5. stream the tiles
@@ -339,6 +304,16 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
     if (k < nsteps) consume(k, wa);
     if (k + 1 < nsteps) consume(k + 1, wb);
     __syncthreads();
+    if constexpr (NORM) {  // per-sequence 1/rms from the waves' sums of squares, in wave order
+        if (tid < B) {
+            float t = 0.0f;
+            for (int w = 0; w < kBgWaves; ++w) t += red[w * 8 + tid];
+            const float tep = t / (float)K;         // rms_kernel.cpp:17
+            const float rms = sqrtf(tep + in.eps);  // :18
+            inv[tid] = 1.0f / rms;                  // :19
+        }
+        __syncthreads();
+    }
     if (in.stamps && tid == 0) {
         unsigned long long* p = in.stamps + (size_t)blockIdx.x * 4;
         p[0] = t_entry;
@@ -351,7 +326,8 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
     if (S == 1) {
         for (int it = tid; it < items; it += kBgThreads) {
             const int j = it >> 6, i = (it >> 3) & 7, b = it & 7;
-            if (b < B) epi.store(t0 + j, i, b, R[j * 128 + i * 8 + b], R[j * 128 + (i + 8) * 8 + b], keys);
+            const float iv = NORM ? inv[b] : 1.0f;
+            if (b < B) epi.store(t0 + j, i, b, R[j * 128 + i * 8 + b] * iv, R[j * 128 + (i + 8) * 8 + b] * iv, keys);
         }
     } else {
         for (int e = tid; e < ntg * 128; e += kBgThreads) {
@@ -509,6 +485,7 @@ hipError_t launch_bgemm(const __half* W, const BgIn& in_, const Epi& epi, const 
     in.tpw = p.tpw;
     in.splits = p.splits;
     const dim3 grid(p.groups * p.splits);
+    if (in.norm_w && p.splits != 1) return hipErrorInvalidValue;  // the fused RMS runs on one split only
     if (in.norm_w)
         hipLaunchKernelGGL((bgemm_kernel<Epi, true>), grid, dim3(kBgThreads), p.lds, s, W, in, epi);
     else

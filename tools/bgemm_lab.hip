@@ -109,7 +109,7 @@ int main(int argc, char** argv) {
         const int sps[] = {1, 2, 4, 8};
         for (int sp : sps)
             for (int tpw : tpws) {
-                if (auto_only) break;
+                if (auto_only || (sh.norm && sp > 1)) break;  // fused-RMS plans run on one split
                 const int nkb = sh.K / 32;
                 if (sp > 1 && nkb / sp < kBgWaves) continue;
                 const int kbs = (nkb + sp - 1) / sp;
