@@ -1,4 +1,4 @@
-"""Tensor parallelism on CPU (gloo, world_size 2 and 4): the shard plan libsli.so uses
+"""Tensor parallelism on CPU (gloo, world_size 2, 4 and 8): the shard plan libsli.so uses
 (sli_tp_plan / sli_tp_vocab) applied to the oracle's weights, the per-rank partial computation the
 engine performs (local heads / FFN columns / vocab rows, residual added on rank 0 only), gloo
 all-reduces where the engine all-reduces over RCCL, and the packed-key distributed argmax. The result
@@ -29,6 +29,15 @@ def _key(val: float, idx: int) -> int:
     return ((ordv << 32) | (0xFFFFFFFF - idx)) - (1 << 63)
 
 
+def _cfg(n_kv):
+    """tiny (MHA, 4 heads), tiny-gqa (4/2) or, for world 8 (config C2's degree), an 8-head MHA variant of
+    the tiny shape (head_dim 32) so every rank owns one head."""
+    from simplellminference_amd.model import preset
+    if n_kv == 8:
+        return preset("tiny", head_dim=32, kv_hidden_size=256, num_attention_heads=8, num_key_value_heads=8)
+    return preset("tiny" if n_kv == 4 else "tiny-gqa")
+
+
 def _worker(rank, world, port, n_kv, out):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -37,10 +46,9 @@ def _worker(rank, world, port, n_kv, out):
 
     import oracle as O
     from simplellminference_amd import tp
-    from simplellminference_amd.model import preset
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    cfg = preset("tiny" if n_kv == 4 else "tiny-gqa")
+    cfg = _cfg(n_kv)
     ocfg = O.Config(cfg.vocab_size, cfg.hidden_size, cfg.num_attention_heads, cfg.num_key_value_heads,
                     cfg.head_dim, cfg.intermediate_size, cfg.num_hidden_layers, cfg.max_length, cfg.rms_norm_eps,
                     cfg.rope_theta)
@@ -96,7 +104,7 @@ def _worker(rank, world, port, n_kv, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n_kv", [(2, 4), (2, 2), (4, 4)])
+@pytest.mark.parametrize("world,n_kv", [(2, 4), (2, 2), (4, 4), (8, 8)])
 def test_tensor_parallel_matches_unsharded_oracle(oracle, world, n_kv):
     from simplellminference_amd import build
     build.build()
@@ -110,8 +118,7 @@ def test_tensor_parallel_matches_unsharded_oracle(oracle, world, n_kv):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    from simplellminference_amd.model import preset
-    cfg = preset("tiny" if n_kv == 4 else "tiny-gqa")
+    cfg = _cfg(n_kv)
     m = oracle.Model(oracle.Config(cfg.vocab_size, cfg.hidden_size, cfg.num_attention_heads, cfg.num_key_value_heads,
                                    cfg.head_dim, cfg.intermediate_size, cfg.num_hidden_layers, cfg.max_length,
                                    cfg.rms_norm_eps, cfg.rope_theta), seed=0)
