@@ -110,3 +110,21 @@ def test_tp_shard_placement_on_device(gpu, oracle, monkeypatch, w, world):
                 assert np.array_equal(m.weight_shard(kind, layer), want), (r, name, layer)
         assert np.array_equal(m.weight_shard(oracle.T_EMB), om.weight(oracle.T_EMB))
         m.close()
+
+
+@pytest.mark.parametrize("w", ["f16", "i8"])
+@pytest.mark.parametrize("world", [2, 8])
+def test_tp_rank_of_c2_shapes_steps_nocomm(gpu, monkeypatch, w, world):
+    """One rank of config C2 (Llama-2-7B shapes, 2 layers, ctx 2048, TP 2 / 8): the rank's GEMV shapes
+    (TP 8: qkv 1536x4096, wo 4096x512, gate/up 2752x4096, down 4096x1376, LM head 4000x4096, 4 heads of
+    attention) plan, allocate and step without a communicator (SLI_DEBUG_NOCOMM: kernel shapes and
+    placement only, the values are not a model); the step is deterministic and idempotent."""
+    from simplellminference_amd.model import LlamaModel, preset
+    monkeypatch.setenv("SLI_DEBUG_NOCOMM", "1")
+    cfg = preset("llama2-7b", num_hidden_layers=2)
+    m = LlamaModel(config=cfg, w_dtype=w, kv_dtype="f16", seed=1, tp_rank=world - 1, tp_size=world).init()
+    m.fill_kv_synthetic(7, 2047)
+    a = m.forward(1234, 2047)
+    b = m.forward(1234, 2047)
+    assert a.shape == (cfg.vocab_size // world,) and np.isfinite(a).all() and np.array_equal(a, b)
+    m.close()
