@@ -1,0 +1,31 @@
+"""Per-rank decode-step time of one tensor-parallel shard on ONE GPU, without a communicator
+(SLI_DEBUG_NOCOMM: the rank's kernels at their real shapes, no RCCL all-reduces; values are not a model).
+Estimates the compute part of config C2 (Llama-2-7B at TP N); the collectives come on top.
+    python tools/tp_rank_time.py [N ...]
+"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ["SLI_DEBUG_NOCOMM"] = "1"
+
+from simplellminference_amd.model import LlamaModel, preset  # noqa: E402
+
+for world in [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]:
+    m = LlamaModel(config=preset("llama2-7b"), w_dtype="f16", kv_dtype="f16", seed=1, tp_rank=world - 1,
+                   tp_size=world).init()
+    m.fill_kv_synthetic(7, 2047)
+    m.set_state(1234, 2047, advance=False)
+    for _ in range(10):
+        m.step()
+    m.sync()
+    t0 = time.perf_counter()
+    n = 50
+    for _ in range(n):
+        m.step()
+    m.sync()
+    ms = 1e3 * (time.perf_counter() - t0) / n
+    print(f"tp{world} rank {world - 1}: {ms:.3f} ms/step compute (no all-reduces)", flush=True)
+    m.close()
