@@ -199,11 +199,37 @@ int sli_model_get_weight(sli_model* m, int32_t kind, int32_t index, float* host,
 int sli_model_stream(sli_model* m, sli_stream_t* out);
 /* Algorithmic HBM bytes of one step on this rank (weights, KV at the current position) — SURVEY.md §8(d). */
 int sli_model_step_bytes(sli_model* m, double* weight_bytes, double* kv_bytes);
+/* ---------------------------------------------------------------- in-process tensor parallelism
+ * The SURVEY.md §4 item-5 "fake communicator" (the reference drives one device, model.cpp:247-256):
+ * tp_size rank models of cfg (cfg->tp_rank is ignored; rank r gets the sli_tp_plan shard of rank r)
+ * on cfg->device, sharing one stream and stepped in lockstep by one captured hipGraph. Every all-reduce
+ * of the multi-GPU step (the residual-stream sum after wo and down, the argmax-key MAX after the LM
+ * head) is a device-side reduction over the ranks' buffers in rank order; the ranks' kernels are the
+ * multi-GPU ones. Rank handles (sli_tp_group_rank) are borrowed: load weights, set state / prompts and
+ * read logits through them; step and destroy only through the group. */
+typedef struct sli_tp_group sli_tp_group;
+int sli_tp_group_create(const sli_model_config* cfg, int32_t tp_size, sli_tp_group** out);
+int sli_tp_group_destroy(sli_tp_group* g);
+int sli_tp_group_rank(sli_tp_group* g, int32_t rank, sli_model** out);
+int sli_tp_group_step(sli_tp_group* g);
+int sli_tp_group_sync(sli_tp_group* g);
+/* sli_model_predict_batch over the group: tokens_out [batch][max_length]; logits_out optional
+ * [max_length][batch][vocab] with the ranks' vocab shards in place (the full vocabulary). */
+int sli_tp_group_predict_batch(sli_tp_group* g, const int32_t* prompts, const int32_t* lens, int32_t ld,
+                               int32_t max_length, int32_t* tokens_out, float* logits_out);
+
 /* Roofline probe: replays the step's weight-streaming (GEMV) kernels `iters` times between HIP events
  * on the model's stream; returns mean device time per GEMV launch, algorithmic bytes per launch and
  * the launches per step. */
 int sli_model_time_gemv(sli_model* m, int32_t iters, double* avg_us, double* bytes_per_launch,
                         int32_t* launches_per_step);
+/* Per-kernel-family probe: for each family f (sli_kernel_family) replays that family's launches of one
+ * step `iters` times between HIP events on the model's stream; us[f] = mean device time per launch,
+ * bytes[f] = algorithmic HBM bytes per launch (the weight matrix (+ int8 row scales),
+ * or K and V of the live context for attention), launches[f] = launches per step. Arrays of
+ * SLI_FAM_COUNT. */
+typedef enum { SLI_FAM_QKV = 0, SLI_FAM_ATTN, SLI_FAM_WO, SLI_FAM_GU, SLI_FAM_DOWN, SLI_FAM_LM, SLI_FAM_COUNT } sli_kernel_family;
+int sli_model_time_families(sli_model* m, int32_t iters, double* us, double* bytes, int32_t* launches);
 
 #ifdef __cplusplus
 }

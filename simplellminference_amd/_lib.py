@@ -97,6 +97,13 @@ _SIGS = {
     "sli_model_stream": (c_int, [c_vp, ctypes.POINTER(c_vp)]),
     "sli_model_step_bytes": (c_int, [c_vp, P_d, P_d]),
     "sli_model_time_gemv": (c_int, [c_vp, c_i32, P_d, P_d, P_i32]),
+    "sli_model_time_families": (c_int, [c_vp, c_i32, P_d, P_d, P_i32]),
+    "sli_tp_group_create": (c_int, [ctypes.POINTER(ModelConfig), c_i32, ctypes.POINTER(c_vp)]),
+    "sli_tp_group_destroy": (c_int, [c_vp]),
+    "sli_tp_group_rank": (c_int, [c_vp, c_i32, ctypes.POINTER(c_vp)]),
+    "sli_tp_group_step": (c_int, [c_vp]),
+    "sli_tp_group_sync": (c_int, [c_vp]),
+    "sli_tp_group_predict_batch": (c_int, [c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp]),
 }
 
 _lib = None

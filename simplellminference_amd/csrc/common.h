@@ -19,6 +19,9 @@ constexpr int kAttnPartPad = 4;
 void set_error(const std::string& msg);
 int fail(int code, const std::string& msg);
 int hip_fail(hipError_t e, const char* what);
+// Compute units of the current device (hipDeviceProp_t::multiProcessorCount, cached per device): every
+// persistent grid is sized from it, never from a hard-coded chip geometry.
+int device_cus();
 
 #define SLI_HIP(expr)                                         \
     do {                                                      \
@@ -123,9 +126,15 @@ template <>
 __device__ __forceinline__ __half from_f32<__half>(float v) { return __float2half_rn(v); }
 
 // Orderable 64-bit argmax key: larger value wins; equal values -> lower index wins (std::max_element's
-// first-max rule, source/op/argmax.cpp:11). Key 0 is below every real key.
+// first-max rule, source/op/argmax.cpp:11, whose scan is `if (*best < *it) best = it`). Key 0 is below
+// every real key. Exactly that scan's result, including the values `<` does not order:
+//   * -0.0 and +0.0 compare equal, so -0.0 is keyed as +0.0 (the earlier of the two wins);
+//   * a NaN never displaces the current best (`best < NaN` is false): key 0, below every number;
+//   * a NaN at index 0 is never displaced either (`NaN < x` is false): the all-ones key, above all.
 __device__ __forceinline__ unsigned long long argmax_key(float v, unsigned idx) {
+    if (v != v) return idx == 0 ? ~0ull : 0ull;
     unsigned u = __float_as_uint(v);
+    u = u == 0x80000000u ? 0u : u;
     unsigned ord = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
     return ((unsigned long long)ord << 32) | (unsigned long long)(0xFFFFFFFFu - idx);
 }

@@ -50,6 +50,8 @@ struct LayerW {
 struct sli_model {
     sli_model_config c{};
     hipStream_t stream = nullptr;
+    bool own_stream = true;  // false for the ranks of an in-process group (they share the group's stream)
+    sli_tp_group* group = nullptr;  // in-process tensor-parallel group this rank belongs to (or null)
     ncclComm_t comm = nullptr;
     bool partial = false;    // wo/down write per-rank partials (+ residual on rank 0) into xpart
     bool collectives = false;  // all-reduce partials / argmax keys over RCCL inside the step
@@ -81,7 +83,21 @@ struct sli_model {
     float* bg_ws = nullptr;               // split-K partials of the batched projections
     unsigned* bg_cnt = nullptr;           // their arrival counters (zero between launches)
     unsigned long long* bkeys = nullptr;  // [B] per-sequence argmax keys (all-reduced MAX under TP)
-    int key_ld = sli::kGemvMaxBlocks;     // per-sequence stride of the per-workgroup argmax keys
+    int key_ld = 0;                       // per-sequence stride of the per-workgroup argmax keys
+};
+
+// In-process tensor parallelism (the "fake communicator"): tp_size rank models on
+// one device share one stream and one captured graph that steps them in lockstep; every all-reduce is a
+// device-side reduction over the ranks' buffers in rank order (the ranks' kernels are the multi-GPU
+// ones, so the sharded engine itself is what the group tests run).
+constexpr int kMaxGroup = 8;
+struct sli_tp_group {
+    int n = 0;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::vector<sli_model*> ranks;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
 };
 
 namespace sli {
@@ -323,6 +339,43 @@ __global__ void get_kv_kernel(const KT* __restrict__ cache, float* out, int hkv,
     }
 }
 
+// ---- in-process group collectives (sli_tp_group)
+struct GroupSumArgs {
+    const float* src[kMaxGroup];  // rank r's partial [B*D] (rank 0's includes the residual)
+    float* dst[kMaxGroup];        // rank r's residual stream x
+    int n_ranks, n;
+};
+
+// x_r = ((p_0 + p_1) + p_2) + ... for every rank r: one fixed order, so every rank holds the same x
+__global__ void __launch_bounds__(256) group_sum_kernel(GroupSumArgs a) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
+        float s = a.src[0][i];
+        for (int r = 1; r < a.n_ranks; ++r) s += a.src[r][i];
+        for (int r = 0; r < a.n_ranks; ++r) a.dst[r][i] = s;
+    }
+}
+
+struct GroupKeyArgs {
+    unsigned long long* key[kMaxGroup];  // rank r's per-sequence argmax keys [B] (batch 1: &st->key)
+    DevState* st[kMaxGroup];
+    const int32_t* prompt[kMaxGroup];
+    int32_t* hist[kMaxGroup];
+    int n_ranks, B, T;
+};
+
+// argmax-key MAX over the ranks' vocab shards (global first max), then every rank's state update
+__global__ void group_finalize_kernel(GroupKeyArgs a) {
+    const int b = threadIdx.x;
+    if (b >= a.B) return;
+    unsigned long long k = 0;
+    for (int r = 0; r < a.n_ranks; ++r) k = a.key[r][b] > k ? a.key[r][b] : k;
+    for (int r = 0; r < a.n_ranks; ++r) {
+        DevState* st = a.st[r] + b;
+        st->key = k;
+        finalize_state(st, a.prompt[r] + (size_t)b * (a.T + 1), a.hist[r] + (size_t)b * (a.T + 1), a.T);
+    }
+}
+
 // ---------------------------------------------------------------- the step
 // Vectors in flight per lane: the per-shape U (fp16, tools/gemv_lab) halved for int8, whose 16-byte
 // vector holds twice the columns: the same columns per chunk, two chunks per 4096-column row instead of
@@ -446,63 +499,117 @@ struct StepRecorder {
         const void* w = wptr(m->emb, m->wbytes, (size_t)m->v_lo * m->D);
         return bg(m, w, bin(m, m->x, m->norms + (size_t)(2 * m->L) * m->D, m->D), e, m->bp_lm);
     }
-    static int record_batched(sli_model* m) {
+    // ---- one step = phases 0 .. 2L (model.cpp:48-139). Phase 2l: [embedding when l = 0,] qkv(l),
+    // attention(l), wo(l); phase 2l+1: gate/up(l), down(l); phase 2L: LM head + first argmax stage.
+    // Under tensor parallelism phases 0 .. 2L-1 end with the sum all-reduce of the residual stream and
+    // phase 2L with the argmax-key MAX exchange; the communicator's recorder (record: none / RCCL;
+    // record_group: the in-process group) places those between the phases.
+    static int record_phase(sli_model* m, int p) {
         hipStream_t s = m->stream;
-        const int eb = std::min(64, (m->D + 255) / 256);
-        hipLaunchKernelGGL(embedding_batch_kernel<WT>, dim3(eb, m->B), dim3(256), 0, s, m->st, (const WT*)m->emb,
-                           m->emb_s, m->x, m->V, m->D);
-        SLI_HIP(hipGetLastError());
-        const long long ps = m->hd, hs = (long long)m->T * m->hd, ls = (long long)m->B * m->hkv * m->T * m->hd;
-        for (int l = 0; l < m->L; ++l) {
-            SLI_TRY(b_qkv(m, l));
-            // the batch is B * hkv kv heads of one layer: sequence b owns kv heads [b*hkv, (b+1)*hkv)
-            SLI_TRY(mha_launch<KT>(m->q, (const KT*)m->kc, (const KT*)m->vc, m->attn, l, 0, &m->st->pos, m->T, m->hd,
-                                   m->B * m->hq, m->B * m->hkv, ps, hs, ls, m->part, m->attn_count, s, m->hkv,
-                                   kPosStride));
-            SLI_TRY(b_wo(m, l));
-            SLI_TRY(allreduce_x(m));
-            SLI_TRY(b_gu(m, l));
-            SLI_TRY(b_down(m, l));
-            SLI_TRY(allreduce_x(m));
+        const bool batched = m->B > 1;
+        if (p == 0) {
+            if (batched) {
+                const int eb = std::min(64, (m->D + 255) / 256);
+                hipLaunchKernelGGL(embedding_batch_kernel<WT>, dim3(eb, m->B), dim3(256), 0, s, m->st,
+                                   (const WT*)m->emb, m->emb_s, m->x, m->V, m->D);
+                SLI_HIP(hipGetLastError());
+            } else {
+                SLI_TRY(embedding_launch(0, &m->st->token, m->emb, m->c.w_dtype, m->emb_s, m->x, m->V, m->D, s));
+            }
         }
-        SLI_TRY(b_lm(m));
-        hipLaunchKernelGGL(keyreduce_batch_kernel, dim3(m->B), dim3(256), 0, s, m->keys, m->key_ld, m->bp_lm.groups,
-                           m->bkeys);
+        if (p >= 2 * m->L) return record_head(m, true);
+        const int l = p / 2;
+        if (p % 2 == 0) {
+            const long long ps = m->hd, hs = (long long)m->T * m->hd;
+            const long long ls = (long long)m->B * m->hkv * m->T * m->hd;
+            SLI_TRY(batched ? b_qkv(m, l) : gemv_qkv(m, l));
+            // a batch is B * hkv kv heads of one layer: sequence b owns kv heads [b*hkv, (b+1)*hkv)
+            SLI_TRY(mha_launch<KT>(m->q, (const KT*)m->kc, (const KT*)m->vc, m->attn, l, 0, &m->st->pos, m->T, m->hd,
+                                   m->B * m->hq, m->B * m->hkv, ps, hs, ls, m->part, m->attn_count, s,
+                                   batched ? m->hkv : 0, batched ? kPosStride : 0));
+            return batched ? b_wo(m, l) : gemv_wo(m, l);
+        }
+        SLI_TRY(batched ? b_gu(m, l) : gemv_gu(m, l));
+        return batched ? b_down(m, l) : gemv_down(m, l);
+    }
+    // LM head + first argmax stage. exchange = false: the step has no cross-rank key exchange, so batch 1
+    // fuses the key reduce with the state update (one launch).
+    static int record_head(sli_model* m, bool exchange) {
+        hipStream_t s = m->stream;
+        if (m->B > 1) {
+            SLI_TRY(b_lm(m));
+            hipLaunchKernelGGL(keyreduce_batch_kernel, dim3(m->B), dim3(256), 0, s, m->keys, m->key_ld,
+                               m->bp_lm.groups, m->bkeys);
+            SLI_HIP(hipGetLastError());
+            return SLI_OK;
+        }
+        SLI_TRY(gemv_lm(m));
+        if (exchange)
+            hipLaunchKernelGGL(keyreduce_kernel<false>, dim3(1), dim3(kKeyThreads), 0, s, m->keys, lm_head_blocks(m),
+                               m->st, m->prompt, m->hist, m->T);
+        else
+            hipLaunchKernelGGL(keyreduce_kernel<true>, dim3(1), dim3(kKeyThreads), 0, s, m->keys, lm_head_blocks(m),
+                               m->st, m->prompt, m->hist, m->T);
         SLI_HIP(hipGetLastError());
-        if (m->collectives) SLI_NCCL(ncclAllReduce(m->bkeys, m->bkeys, m->B, ncclUint64, ncclMax, m->comm, s));
-        hipLaunchKernelGGL(finalize_batch_kernel, dim3(1), dim3(64), 0, s, m->st, m->bkeys, m->prompt, m->hist, m->T,
-                           m->B);
+        return SLI_OK;
+    }
+    // state update after the (exchanged) argmax keys: position, next token, history (model.cpp:157-183)
+    static int record_finalize(sli_model* m) {
+        hipStream_t s = m->stream;
+        if (m->B > 1)
+            hipLaunchKernelGGL(finalize_batch_kernel, dim3(1), dim3(64), 0, s, m->st, m->bkeys, m->prompt, m->hist,
+                               m->T, m->B);
+        else
+            hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1), 0, s, m->st, m->prompt, m->hist, m->T);
         SLI_HIP(hipGetLastError());
         return SLI_OK;
     }
 
+    // one model and its own communicator (none, RCCL, or the debug modes)
     static int record(sli_model* m) {
-        if (m->B > 1) return record_batched(m);
-        hipStream_t s = m->stream;
-        SLI_TRY(embedding_launch(0, &m->st->token, m->emb, m->c.w_dtype, m->emb_s, m->x, m->V, m->D, s));
-        const long long ps = m->hd, hs = (long long)m->T * m->hd, ls = (long long)m->hkv * m->T * m->hd;
-        for (int l = 0; l < m->L; ++l) {
-            SLI_TRY(gemv_qkv(m, l));
-            SLI_TRY(mha_launch<KT>(m->q, (const KT*)m->kc, (const KT*)m->vc, m->attn, l, 0, &m->st->pos, m->T, m->hd,
-                                   m->hq, m->hkv, ps, hs, ls, m->part, m->attn_count, s));
-            SLI_TRY(gemv_wo(m, l));
-            SLI_TRY(allreduce_x(m));
-            SLI_TRY(gemv_gu(m, l));
-            SLI_TRY(gemv_down(m, l));
+        for (int p = 0; p < 2 * m->L; ++p) {
+            SLI_TRY(record_phase(m, p));
             SLI_TRY(allreduce_x(m));
         }
-        SLI_TRY(gemv_lm(m));
         if (!m->collectives) {
-            hipLaunchKernelGGL(keyreduce_kernel<true>, dim3(1), dim3(kKeyThreads), 0, s, m->keys, lm_head_blocks(m),
-                               m->st, m->prompt, m->hist, m->T);
-            SLI_HIP(hipGetLastError());
-            return SLI_OK;
+            SLI_TRY(record_head(m, m->B > 1));
+            return m->B > 1 ? record_finalize(m) : SLI_OK;
         }
-        hipLaunchKernelGGL(keyreduce_kernel<false>, dim3(1), dim3(kKeyThreads), 0, s, m->keys, lm_head_blocks(m), m->st,
-                           m->prompt, m->hist, m->T);
-        SLI_HIP(hipGetLastError());
-        SLI_NCCL(ncclAllReduce(&m->st->key, &m->st->key, 1, ncclUint64, ncclMax, m->comm, s));
-        hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1), 0, s, m->st, m->prompt, m->hist, m->T);
+        SLI_TRY(record_head(m, true));
+        if (m->B > 1)
+            SLI_NCCL(ncclAllReduce(m->bkeys, m->bkeys, m->B, ncclUint64, ncclMax, m->comm, m->stream));
+        else
+            SLI_NCCL(ncclAllReduce(&m->st->key, &m->st->key, 1, ncclUint64, ncclMax, m->comm, m->stream));
+        return record_finalize(m);
+    }
+    // the in-process group: phase p of every rank, then the device-side collective (sli_tp_group)
+    static int record_group(sli_tp_group* g) {
+        sli_model* m0 = g->ranks[0];
+        const int n = g->n;
+        GroupSumArgs sa{};
+        sa.n_ranks = n;
+        sa.n = m0->B * m0->D;
+        GroupKeyArgs ka{};
+        ka.n_ranks = n;
+        ka.B = m0->B;
+        ka.T = m0->T;
+        for (int r = 0; r < n; ++r) {
+            sli_model* m = g->ranks[r];
+            sa.src[r] = m->xpart;
+            sa.dst[r] = m->x;
+            ka.key[r] = m->B > 1 ? m->bkeys : &m->st->key;
+            ka.st[r] = m->st;
+            ka.prompt[r] = m->prompt;
+            ka.hist[r] = m->hist;
+        }
+        const int blocks = std::min(64, (sa.n + 255) / 256);
+        for (int p = 0; p < 2 * m0->L; ++p) {
+            for (int r = 0; r < n; ++r) SLI_TRY(record_phase(g->ranks[r], p));
+            hipLaunchKernelGGL(group_sum_kernel, dim3(blocks), dim3(256), 0, g->stream, sa);
+            SLI_HIP(hipGetLastError());
+        }
+        for (int r = 0; r < n; ++r) SLI_TRY(record_head(g->ranks[r], true));
+        hipLaunchKernelGGL(group_finalize_kernel, dim3(1), dim3(64), 0, g->stream, ka);
         SLI_HIP(hipGetLastError());
         return SLI_OK;
     }
@@ -524,6 +631,30 @@ struct StepRecorder {
             SLI_TRY(gemv_down(m, l));
         }
         return gemv_lm(m);
+    }
+    // The launches of one kernel family in one step (for the per-family timing probe): every layer's
+    // qkv / attention / wo / gate-up / down launch, or the LM head.
+    static int family(sli_model* m, int f) {
+        const bool batched = m->B > 1;
+        if (f == SLI_FAM_LM) return batched ? b_lm(m) : gemv_lm(m);
+        for (int l = 0; l < m->L; ++l) {
+            switch (f) {
+                case SLI_FAM_QKV: SLI_TRY(batched ? b_qkv(m, l) : gemv_qkv(m, l)); break;
+                case SLI_FAM_ATTN: {
+                    const long long ps = m->hd, hs = (long long)m->T * m->hd;
+                    const long long ls = (long long)m->B * m->hkv * m->T * m->hd;
+                    SLI_TRY(mha_launch<KT>(m->q, (const KT*)m->kc, (const KT*)m->vc, m->attn, l, 0, &m->st->pos, m->T,
+                                           m->hd, m->B * m->hq, m->B * m->hkv, ps, hs, ls, m->part, m->attn_count,
+                                           m->stream, batched ? m->hkv : 0, batched ? kPosStride : 0));
+                    break;
+                }
+                case SLI_FAM_WO: SLI_TRY(batched ? b_wo(m, l) : gemv_wo(m, l)); break;
+                case SLI_FAM_GU: SLI_TRY(batched ? b_gu(m, l) : gemv_gu(m, l)); break;
+                case SLI_FAM_DOWN: SLI_TRY(batched ? b_down(m, l) : gemv_down(m, l)); break;
+                default: return fail(SLI_ERR_ARG, "unknown kernel family");
+            }
+        }
+        return SLI_OK;
     }
     static int fill_kv(sli_model* m, uint32_t seed, int upto) {
         const uint64_t n = (uint64_t)m->L * m->B * m->hkv * upto * m->hd;
@@ -553,20 +684,30 @@ struct StepRecorder {
         return StepRecorder<int8_t, float>::FN(__VA_ARGS__);                                            \
     })()
 
-static int capture(sli_model* m) {
-    if (m->graph_exec) return SLI_OK;
-    SLI_HIP(hipStreamBeginCapture(m->stream, hipStreamCaptureModeRelaxed));
-    int rc = SLI_DISPATCH(m, record, m);
+template <class Rec>
+static int capture_graph(hipStream_t stream, hipGraph_t& graph, hipGraphExec_t& exec, Rec record) {
+    if (exec) return SLI_OK;
+    SLI_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed));
+    int rc = record();
     hipGraph_t g = nullptr;
-    hipError_t e = hipStreamEndCapture(m->stream, &g);
+    hipError_t e = hipStreamEndCapture(stream, &g);
     if (rc != SLI_OK) {
         if (g) (void)hipGraphDestroy(g);
         return rc;
     }
     if (e != hipSuccess) return hip_fail(e, "hipStreamEndCapture");
-    m->graph = g;
-    SLI_HIP(hipGraphInstantiate(&m->graph_exec, g, nullptr, nullptr, 0));
+    graph = g;
+    SLI_HIP(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
     return SLI_OK;
+}
+
+static int capture(sli_model* m) {
+    return capture_graph(m->stream, m->graph, m->graph_exec, [&]() { return SLI_DISPATCH(m, record, m); });
+}
+
+static int capture_group(sli_tp_group* g) {
+    sli_model* m0 = g->ranks[0];
+    return capture_graph(g->stream, g->graph, g->exec, [&]() { return SLI_DISPATCH(m0, record_group, g); });
 }
 
 static int upload_states(sli_model* m, const std::vector<DevState>& h) {
@@ -590,7 +731,7 @@ static void destroy(sli_model* m) {
     if (m->graph) (void)hipGraphDestroy(m->graph);
     if (m->comm) ncclCommDestroy(m->comm);
     for (void* p : m->allocs) (void)hipFree(p);
-    if (m->stream) (void)hipStreamDestroy(m->stream);
+    if (m->stream && m->own_stream) (void)hipStreamDestroy(m->stream);
     delete m;
 }
 
@@ -610,7 +751,8 @@ int sli_comm_get_id(void* out) {
     return SLI_OK;
 }
 
-int sli_model_create(const sli_model_config* cfg, const void* comm_id, sli_model** out) {
+// group != null: rank cfg->tp_rank of an in-process group (shares the group's stream, no communicator)
+static int create_model(const sli_model_config* cfg, const void* comm_id, sli_tp_group* group, sli_model** out) {
     SLI_CHECK(cfg && out, SLI_ERR_ARG, "sli_model_create: null");
     const sli_model_config& c = *cfg;
     SLI_CHECK(c.vocab > 0 && c.dim > 0 && c.n_heads > 0 && c.n_kv_heads > 0 && c.head_dim > 0 && c.ffn > 0 &&
@@ -627,7 +769,7 @@ int sli_model_create(const sli_model_config* cfg, const void* comm_id, sli_model
     SLI_CHECK((c.ffn / c.tp_size) % 2 == 0, SLI_ERR_SHAPE, "local ffn must be even");
     SLI_CHECK(c.w_dtype >= SLI_DT_F32 && c.w_dtype <= SLI_DT_I8, SLI_ERR_ARG, "bad w_dtype");
     SLI_CHECK(c.kv_dtype == SLI_DT_F32 || c.kv_dtype == SLI_DT_F16, SLI_ERR_ARG, "bad kv_dtype");
-    SLI_CHECK(c.tp_size == 1 || comm_id || std::getenv("SLI_DEBUG_NOCOMM"), SLI_ERR_ARG,
+    SLI_CHECK(c.tp_size == 1 || comm_id || group || std::getenv("SLI_DEBUG_NOCOMM"), SLI_ERR_ARG,
               "tensor parallel needs a comm id");
     const size_t wb = c.w_dtype == SLI_DT_F32 ? 4 : c.w_dtype == SLI_DT_F16 ? 2 : 1;
     SLI_CHECK(((size_t)c.dim * wb) % 16 == 0 && ((size_t)(c.ffn / c.tp_size) * wb) % 16 == 0 &&
@@ -650,8 +792,13 @@ int sli_model_create(const sli_model_config* cfg, const void* comm_id, sli_model
         destroy(m);
         return rc;
     };
-    if (hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess)
+    if (group) {
+        m->stream = group->stream;
+        m->own_stream = false;
+        m->group = group;
+    } else if (hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess) {
         return bail(fail(SLI_ERR_HIP, "hipStreamCreate"));
+    }
     m->B = B;
     m->D = c.dim;
     m->L = c.n_layers;
@@ -704,18 +851,20 @@ int sli_model_create(const sli_model_config* cfg, const void* comm_id, sli_model
     A((void**)&m->attn_count, sizeof(unsigned) * B * m->hkv);   // per-kv-head arrival counters (kept zero)
     size_t bg_part = 0;
     int bg_groups = 1;
+    const int cus = device_cus();
+    m->key_ld = gemv_max_blocks();  // LM-head argmax keys: one per GEMV workgroup
     if (B > 1) {  // tilings of the batched projections (bgemm.h)
-        m->bp_qkv = bg_plan(qkv_rows / 16, D, B, true);
-        m->bp_wo = bg_plan((D + 15) / 16, m->hq * hd, B, false);
-        m->bp_gu = bg_plan(m->Il / 8, D, B, true);
-        m->bp_down = bg_plan((D + 15) / 16, m->Il, B, false);
-        m->bp_lm = bg_plan((m->v_n + 15) / 16, D, B, true);
+        m->bp_qkv = bg_plan(qkv_rows / 16, D, B, true, cus);
+        m->bp_wo = bg_plan((D + 15) / 16, m->hq * hd, B, false, cus);
+        m->bp_gu = bg_plan(m->Il / 8, D, B, true, cus);
+        m->bp_down = bg_plan((D + 15) / 16, m->Il, B, false, cus);
+        m->bp_lm = bg_plan((m->v_n + 15) / 16, D, B, true, cus);
         for (const BgPlan* p : {&m->bp_qkv, &m->bp_wo, &m->bp_gu, &m->bp_down, &m->bp_lm}) {
             if (p->groups <= 0) return bail(fail(SLI_ERR_SHAPE, "batched projection: no tiling fits"));
             bg_part = std::max(bg_part, bg_part_bytes(*p));
             bg_groups = std::max(bg_groups, p->groups);
         }
-        m->key_ld = std::max(kGemvMaxBlocks, m->bp_lm.groups);
+        m->key_ld = std::max(m->key_ld, m->bp_lm.groups);
         A((void**)&m->bg_ws, bg_part + 256);
         A((void**)&m->bg_cnt, sizeof(unsigned) * bg_groups);
     }
@@ -745,10 +894,10 @@ int sli_model_create(const sli_model_config* cfg, const void* comm_id, sli_model
     // Debug switches (tests only): SLI_DEBUG_FORCE_COMM=1 runs the tensor-parallel step
     // (partials + RCCL all-reduces) on a 1-rank communicator; SLI_DEBUG_NOCOMM=1 builds a tp_size>1
     // shard without a communicator (weight-placement checks; its logits are not meaningful).
-    const bool force_comm = c.tp_size == 1 && std::getenv("SLI_DEBUG_FORCE_COMM") != nullptr;
-    const bool no_comm = c.tp_size > 1 && std::getenv("SLI_DEBUG_NOCOMM") != nullptr;
-    m->partial = c.tp_size > 1 || force_comm;
-    m->collectives = (c.tp_size > 1 && !no_comm) || force_comm;
+    const bool force_comm = !group && c.tp_size == 1 && std::getenv("SLI_DEBUG_FORCE_COMM") != nullptr;
+    const bool no_comm = !group && c.tp_size > 1 && std::getenv("SLI_DEBUG_NOCOMM") != nullptr;
+    m->partial = c.tp_size > 1 || force_comm || group;
+    m->collectives = !group && ((c.tp_size > 1 && !no_comm) || force_comm);  // a group's are its own kernels
     if (m->collectives) {
         ncclUniqueId id;
         if (comm_id) {
@@ -763,7 +912,12 @@ int sli_model_create(const sli_model_config* cfg, const void* comm_id, sli_model
     return SLI_OK;
 }
 
+int sli_model_create(const sli_model_config* cfg, const void* comm_id, sli_model** out) {
+    return create_model(cfg, comm_id, nullptr, out);
+}
+
 int sli_model_destroy(sli_model* m) {
+    SLI_CHECK(!m || !m->group, SLI_ERR_STATE, "a rank of an in-process tp group is destroyed with its group");
     destroy(m);
     return SLI_OK;
 }
@@ -941,6 +1095,7 @@ int sli_model_get_history(sli_model* m, int32_t seq, int32_t n, int32_t* out) {
 
 int sli_model_step(sli_model* m) {
     SLI_CHECK(m, SLI_ERR_ARG, "null model");
+    SLI_CHECK(!m->group, SLI_ERR_STATE, "a rank of an in-process tp group steps with its group (sli_tp_group_step)");
     SLI_TRY(capture(m));
     SLI_HIP(hipGraphLaunch(m->graph_exec, m->stream));
     return SLI_OK;
@@ -1088,29 +1243,90 @@ int sli_model_step_bytes(sli_model* m, double* weight_bytes, double* kv_bytes) {
     return SLI_OK;
 }
 
+int sli_model_time_families(sli_model* m, int32_t iters, double* us, double* bytes, int32_t* launches) {
+    SLI_CHECK(m && iters > 0 && us && bytes && launches, SLI_ERR_ARG, "bad argument");
+    SLI_CHECK(!m->group, SLI_ERR_STATE, "time a group's ranks through a standalone model");
+    SLI_HIP(hipSetDevice(m->c.device));
+    // Like sli_model_time_gemv: x is saved and restored; the qkv family rewrites each layer's K/V row at
+    // the current position, which the next real step at that position rewrites again.
+    struct Guard {
+        float* xsave = nullptr;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        ~Guard() {
+            if (xsave) (void)hipFree(xsave);
+            if (e0) (void)hipEventDestroy(e0);
+            if (e1) (void)hipEventDestroy(e1);
+        }
+    } g;
+    const size_t xb = sizeof(float) * m->B * m->D;
+    SLI_HIP(hipMalloc(&g.xsave, xb));
+    SLI_HIP(hipMemcpyAsync(g.xsave, m->x, xb, hipMemcpyDeviceToDevice, m->stream));
+    SLI_HIP(hipEventCreate(&g.e0));
+    SLI_HIP(hipEventCreate(&g.e1));
+    std::vector<DevState> h;
+    SLI_TRY(download_states(m, h));
+    double ctx = 0.0;
+    for (const DevState& d : h) ctx += d.pos + 1.0;
+    const double wb = (double)m->wbytes, D = m->D, hd = m->hd, i8 = m->c.w_dtype == SLI_DT_I8 ? 4.0 : 0.0;
+    const double qkv_rows = (m->hq + 2.0 * m->hkv) * hd;
+    bytes[SLI_FAM_QKV] = qkv_rows * (D * wb + i8);
+    bytes[SLI_FAM_ATTN] = 2.0 * ctx * m->hkv * hd * (double)m->kvbytes;
+    bytes[SLI_FAM_WO] = D * (m->hq * hd * wb + i8);
+    bytes[SLI_FAM_GU] = 2.0 * m->Il * (D * wb + i8);
+    bytes[SLI_FAM_DOWN] = D * (m->Il * wb + i8);
+    bytes[SLI_FAM_LM] = (double)m->v_n * (D * wb + i8);
+    int rc = SLI_OK;
+    for (int f = 0; rc == SLI_OK && f < SLI_FAM_COUNT; ++f) {
+        launches[f] = f == SLI_FAM_LM ? 1 : m->L;
+        rc = SLI_DISPATCH(m, family, m, f);  // warm-up
+        if (rc == SLI_OK && hipEventRecord(g.e0, m->stream) != hipSuccess) rc = fail(SLI_ERR_HIP, "event");
+        for (int i = 0; rc == SLI_OK && i < iters; ++i) rc = SLI_DISPATCH(m, family, m, f);
+        if (rc == SLI_OK && hipEventRecord(g.e1, m->stream) != hipSuccess) rc = fail(SLI_ERR_HIP, "event");
+        float ms = 0.0f;
+        if (rc == SLI_OK &&
+            (hipEventSynchronize(g.e1) != hipSuccess || hipEventElapsedTime(&ms, g.e0, g.e1) != hipSuccess))
+            rc = fail(SLI_ERR_HIP, "event timing");
+        us[f] = 1000.0 * ms / ((double)iters * launches[f]);
+    }
+    if (hipMemcpyAsync(m->x, g.xsave, xb, hipMemcpyDeviceToDevice, m->stream) != hipSuccess ||
+        hipStreamSynchronize(m->stream) != hipSuccess) {
+        if (rc == SLI_OK) rc = fail(SLI_ERR_HIP, "restore x");
+    }
+    return rc;
+}
+
 int sli_model_time_gemv(sli_model* m, int32_t iters, double* avg_us, double* bytes_per_launch,
                         int32_t* launches_per_step) {
     SLI_CHECK(m && iters > 0, SLI_ERR_ARG, "bad argument");
     SLI_HIP(hipSetDevice(m->c.device));
-    // the probe re-runs the step's GEMVs in place: save and restore the residual stream
-    float* xsave = nullptr;
-    SLI_HIP(hipMalloc(&xsave, sizeof(float) * m->B * m->D));
-    SLI_HIP(hipMemcpyAsync(xsave, m->x, sizeof(float) * m->B * m->D, hipMemcpyDeviceToDevice, m->stream));
-    hipEvent_t e0, e1;
-    SLI_HIP(hipEventCreate(&e0));
-    SLI_HIP(hipEventCreate(&e1));
+    // The probe re-runs the step's weight-streaming launches in place. It saves and restores the residual
+    // stream x; its QKV launches rewrite each layer's K/V row at the current position (from the final x),
+    // which the next real step at that position overwrites again (the bench's idempotent step does).
+    struct Guard {  // every exit path frees the save buffer and both events
+        float* xsave = nullptr;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        ~Guard() {
+            if (xsave) (void)hipFree(xsave);
+            if (e0) (void)hipEventDestroy(e0);
+            if (e1) (void)hipEventDestroy(e1);
+        }
+    } g;
+    const size_t xb = sizeof(float) * m->B * m->D;
+    SLI_HIP(hipMalloc(&g.xsave, xb));
+    SLI_HIP(hipMemcpyAsync(g.xsave, m->x, xb, hipMemcpyDeviceToDevice, m->stream));
+    SLI_HIP(hipEventCreate(&g.e0));
+    SLI_HIP(hipEventCreate(&g.e1));
     int rc = SLI_DISPATCH(m, gemvs, m);  // warm-up
-    if (rc == SLI_OK) SLI_HIP(hipEventRecord(e0, m->stream));
+    if (rc == SLI_OK) rc = hipEventRecord(g.e0, m->stream) == hipSuccess ? SLI_OK : fail(SLI_ERR_HIP, "event");
     for (int i = 0; rc == SLI_OK && i < iters; ++i) rc = SLI_DISPATCH(m, gemvs, m);
-    if (rc == SLI_OK) SLI_HIP(hipEventRecord(e1, m->stream));
-    SLI_HIP(hipEventSynchronize(e1));
+    if (rc == SLI_OK) rc = hipEventRecord(g.e1, m->stream) == hipSuccess ? SLI_OK : fail(SLI_ERR_HIP, "event");
     float ms = 0.0f;
-    SLI_HIP(hipEventElapsedTime(&ms, e0, e1));
-    SLI_HIP(hipMemcpyAsync(m->x, xsave, sizeof(float) * m->B * m->D, hipMemcpyDeviceToDevice, m->stream));
-    SLI_HIP(hipStreamSynchronize(m->stream));
-    (void)hipFree(xsave);
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
+    if (rc == SLI_OK && (hipEventSynchronize(g.e1) != hipSuccess || hipEventElapsedTime(&ms, g.e0, g.e1) != hipSuccess))
+        rc = fail(SLI_ERR_HIP, "event timing");
+    if (hipMemcpyAsync(m->x, g.xsave, xb, hipMemcpyDeviceToDevice, m->stream) != hipSuccess ||
+        hipStreamSynchronize(m->stream) != hipSuccess) {
+        if (rc == SLI_OK) rc = fail(SLI_ERR_HIP, "restore x");
+    }
     if (rc != SLI_OK) return rc;
     const int n_launch = 4 * m->L + 1;
     double wbytes = 0.0;
@@ -1118,6 +1334,97 @@ int sli_model_time_gemv(sli_model* m, int32_t iters, double* avg_us, double* byt
     if (avg_us) *avg_us = 1000.0 * ms / ((double)iters * n_launch);
     if (bytes_per_launch) *bytes_per_launch = wbytes / n_launch;
     if (launches_per_step) *launches_per_step = n_launch;
+    return SLI_OK;
+}
+
+// ---------------------------------------------------------------- in-process tensor-parallel group
+int sli_tp_group_create(const sli_model_config* cfg, int32_t tp_size, sli_tp_group** out) {
+    SLI_CHECK(cfg && out, SLI_ERR_ARG, "sli_tp_group_create: null");
+    SLI_CHECK(tp_size >= 1 && tp_size <= kMaxGroup, SLI_ERR_ARG, "tp group size must be in [1, 8]");
+    SLI_HIP(hipSetDevice(cfg->device));
+    sli_tp_group* g = new sli_tp_group();
+    g->n = tp_size;
+    g->device = cfg->device;
+    if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete g;
+        return fail(SLI_ERR_HIP, "hipStreamCreate");
+    }
+    for (int r = 0; r < tp_size; ++r) {
+        sli_model_config c = *cfg;
+        c.tp_rank = r;
+        c.tp_size = tp_size;
+        sli_model* m = nullptr;
+        const int rc = create_model(&c, nullptr, g, &m);
+        if (rc != SLI_OK) {
+            const std::string err = sli_last_error();
+            sli_tp_group_destroy(g);
+            return fail(rc, err);
+        }
+        g->ranks.push_back(m);
+    }
+    *out = g;
+    return SLI_OK;
+}
+
+int sli_tp_group_destroy(sli_tp_group* g) {
+    if (!g) return SLI_OK;
+    (void)hipSetDevice(g->device);
+    if (g->stream) (void)hipStreamSynchronize(g->stream);
+    if (g->exec) (void)hipGraphExecDestroy(g->exec);
+    if (g->graph) (void)hipGraphDestroy(g->graph);
+    for (sli_model* m : g->ranks) destroy(m);
+    if (g->stream) (void)hipStreamDestroy(g->stream);
+    delete g;
+    return SLI_OK;
+}
+
+int sli_tp_group_rank(sli_tp_group* g, int32_t rank, sli_model** out) {
+    SLI_CHECK(g && out, SLI_ERR_ARG, "null argument");
+    SLI_CHECK(rank >= 0 && rank < g->n, SLI_ERR_RANGE, "rank out of range");
+    *out = g->ranks[rank];
+    return SLI_OK;
+}
+
+int sli_tp_group_step(sli_tp_group* g) {
+    SLI_CHECK(g, SLI_ERR_ARG, "null group");
+    SLI_HIP(hipSetDevice(g->device));
+    SLI_TRY(capture_group(g));
+    SLI_HIP(hipGraphLaunch(g->exec, g->stream));
+    return SLI_OK;
+}
+
+int sli_tp_group_sync(sli_tp_group* g) {
+    SLI_CHECK(g, SLI_ERR_ARG, "null group");
+    SLI_HIP(hipStreamSynchronize(g->stream));
+    return SLI_OK;
+}
+
+int sli_tp_group_predict_batch(sli_tp_group* g, const int32_t* prompts, const int32_t* lens, int32_t ld,
+                               int32_t max_length, int32_t* tokens_out, float* logits_out) {
+    SLI_CHECK(g && prompts && lens && tokens_out, SLI_ERR_ARG, "null argument");
+    sli_model* m0 = g->ranks[0];
+    SLI_CHECK(max_length >= 1 && max_length <= m0->T, SLI_ERR_RANGE, "max_length must be in [1, max_len]");
+    for (sli_model* m : g->ranks) {
+        for (int b = 0; b < m->B; ++b) {
+            SLI_CHECK(lens[b] >= 1 && lens[b] <= ld, SLI_ERR_RANGE, "prompt length out of range");
+            SLI_TRY(set_prompt(m, b, prompts + (size_t)b * ld, lens[b]));
+            SLI_TRY(set_state(m, b, prompts[(size_t)b * ld], 0, 1));
+        }
+    }
+    const int B = m0->B, V = m0->V;
+    for (int t = 0; t < max_length; ++t) {  // model.cpp:157
+        SLI_TRY(sli_tp_group_step(g));
+        if (!logits_out) continue;
+        for (sli_model* m : g->ranks)  // [t][b][v_lo .. v_lo + v_n) <- rank's [b][v_n]
+            SLI_HIP(hipMemcpy2DAsync(logits_out + ((size_t)t * B) * V + m->v_lo, sizeof(float) * V, m->logits,
+                                     sizeof(float) * m->v_n, sizeof(float) * m->v_n, B, hipMemcpyDeviceToHost,
+                                     g->stream));
+        SLI_HIP(hipStreamSynchronize(g->stream));
+    }
+    for (int b = 0; b < B; ++b)
+        SLI_HIP(hipMemcpyAsync(tokens_out + (size_t)b * max_length, m0->hist + (size_t)b * (m0->T + 1),
+                               sizeof(int32_t) * max_length, hipMemcpyDeviceToHost, g->stream));
+    SLI_HIP(hipStreamSynchronize(g->stream));
     return SLI_OK;
 }
 

@@ -387,9 +387,11 @@ struct EpiQKV {
         pre_pos = *pos_dev;
         int r[2];
         rows(u, r);
+        // without row scales: an unconditional load of a known-valid element (sin_t[0]), never a row
+        // index into the [T][hd/2] table
         const float* sp = rscale ? rscale : sin_t;
-        pre_s0 = sp[r[0]];
-        pre_s1 = sp[r[1]];
+        pre_s0 = sp[rscale ? r[0] : 0];
+        pre_s1 = sp[rscale ? r[1] : 0];
     }
     // after the input commit (the position has landed with the input): the table row of this position
     __device__ void prefetch_b(int u) {
@@ -531,14 +533,15 @@ struct EpiLogits {
 namespace sli {
 
 constexpr int kGemvMaxCols = 16384 - kGemvLdsHead;  // x staged in 64 KiB of LDS (<= kGemvThreads*4*kGemvStageV4)
-constexpr int kGemvCUs = 256;                                  // MI355X: 8 XCDs x 32 CUs
-constexpr int kGemvMaxBlocks = kGemvCUs;                       // persistent grid: one workgroup per CU
+// persistent grid: one workgroup per CU of the current device (MI355X: 8 XCDs x 32 CUs = 256)
+inline int gemv_max_blocks() { return device_cus(); }
 
 // Grid: enough workgroups for every unit to have a wave, capped at the persistent size; the balanced
 // schedule in gemv_kernel spreads the units over whatever grid this returns.
 inline int gemv_blocks(int units) {
+    const int maxb = gemv_max_blocks();
     int b = (units + (kGemvThreads / 64) - 1) / (kGemvThreads / 64);
-    return b < kGemvMaxBlocks ? (b > 0 ? b : 1) : kGemvMaxBlocks;
+    return b < maxb ? (b > 0 ? b : 1) : maxb;
 }
 
 template <typename WT, int R, int U, bool NT, class Epi>

@@ -68,7 +68,7 @@ void mha_kernel_cuda_ws(const mem::Tensor& query, const mem::Tensor& key_cache, 
 }
 
 // Reference signature: `score` ({head_dim, max_seq_len} scratch, model.cpp:279) doubles as the
-// split-context workspace when large enough; otherwise a cached device workspace is used.
+// split-context workspace when large enough; otherwise a per-call allocator scratch is used.
 void mha_kernel_cuda(const mem::Tensor& query, const mem::Tensor& score, const mem::Tensor& key_cache,
                      const mem::Tensor& value_cache, const mem::Tensor& mha_out, int32_t layer_index, int32_t pos,
                      int32_t max_seq_len, int32_t head_dim, int32_t hidden_dim, int32_t kv_hidden_dim,
@@ -83,9 +83,11 @@ void mha_kernel_cuda(const mem::Tensor& query, const mem::Tensor& score, const m
                            num_attention_heads, kvh, score);
         return;
     }
-    static thread_local mem::Tensor ws;
-    if (ws.byte_size() < need)
-        ws = mem::Tensor({(int32_t)((need + 3) / 4)}, true, mem::CUDADeviceAllocatorFactory::get_instance());
+    // A score buffer too small for the split partials (more than ~16384/(hd+4) heads): a per-call scratch
+    // from the device allocator, returned to its pool when this call returns. Every kernel-level op runs on
+    // the default stream, so a later reuse of the block is ordered behind this launch (the reference's own
+    // per-call RMSNorm scratch follows the same pattern, rms_kernel.cu:48-51).
+    mem::Tensor ws({(int32_t)((need + 3) / 4)}, true, mem::CUDADeviceAllocatorFactory::get_instance());
     mha_kernel_cuda_ws(query, key_cache, value_cache, mha_out, layer_index, pos, max_seq_len, head_dim,
                        num_attention_heads, kvh, ws);
 }

@@ -213,9 +213,8 @@ argmaxLayer::argmaxLayer(base::DeviceType d, int32_t hidden_dim_size) : device_t
 void argmaxLayer::forward(const mem::Tensor& logits, const mem::Tensor& input_idx) {
     int32_t* dst = const_cast<int32_t*>(input_idx.ptr<int32_t>());
     if (logits.device_type() == base::DeviceType::kDeviceCUDA) {
-        static thread_local mem::Tensor scratch;
-        if (scratch.is_empty())
-            scratch = mem::Tensor({1}, base::DataType::kFp32, true, mem::CUDADeviceAllocatorFactory::get_instance());
+        // per-call device scratch from the allocator pool (the copy below synchronises before it returns)
+        mem::Tensor scratch({1}, base::DataType::kFp32, true, mem::CUDADeviceAllocatorFactory::get_instance());
         int32_t* d = scratch.ptr<int32_t>();
         if (sli_argmax(logits.ptr<float>(), hidden_dim_size_, d, nullptr) != SLI_OK) LOG(sli_last_error());
         if (input_idx.device_type() == base::DeviceType::kDeviceCUDA) {

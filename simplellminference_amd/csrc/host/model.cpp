@@ -6,6 +6,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <iostream>
 #include <sstream>
 
@@ -119,8 +120,13 @@ std::vector<int32_t> LlamaModel::predict_ids(const std::vector<int32_t>& prompt,
                                              std::vector<float>* logits) {
     if (prompt.empty()) LOG("empty prompt");
     std::vector<int32_t> toks(max_length);
+    // rows of the returned logits are this rank's actual vocab shard (the engine's row stride), which is
+    // shorter than ceil(V / tp) on the last rank when tp_size does not divide the vocab
+    int32_t lo = 0, vn = 0;
     const int32_t chunk = (config_->vocab_size + options_.tp_size - 1) / options_.tp_size;
-    if (logits) logits->assign((size_t)max_length * chunk, 0.0f);
+    lo = std::min(config_->vocab_size, options_.tp_rank * chunk);
+    vn = std::max(0, std::min(chunk, config_->vocab_size - lo));
+    if (logits) logits->assign((size_t)max_length * vn, 0.0f);
     check(sli_model_predict(engine_, prompt.data(), (int32_t)prompt.size(), max_length, toks.data(),
                             logits ? logits->data() : nullptr),
           "sli_model_predict");

@@ -147,7 +147,7 @@ static int matmul_dispatch(const float* x, const WT* w, const float* rscale, flo
         GemvIn in{x, nullptr, 0.0f, cols};
         SLI_HIP((launch_gemv<WT, 2, 4, true>(w, in, epi, (rows + 1) / 2, s)));
     } else {
-        const int blocks = std::min(kGemvMaxBlocks, (rows + 3) / 4);
+        const int blocks = std::min(gemv_max_blocks(), (rows + 3) / 4);
         hipLaunchKernelGGL(gemv_scalar_kernel<WT>, dim3(blocks), dim3(kGemvThreads), 0, s, w, x, rscale, y, rows,
                            cols, scale);
         SLI_HIP(hipGetLastError());
@@ -253,7 +253,7 @@ int sli_matmul(const float* x, const void* w, int w_dtype, const float* w_row_sc
 
 size_t sli_matmul_batch_workspace_bytes(int32_t rows, int32_t cols, int32_t batch) {
     if (rows <= 0 || cols <= 0 || batch <= 0 || batch > kBgMaxBatch || cols % 32 != 0) return 0;
-    return bg_ws_bytes(bg_plan((rows + 15) / 16, cols, batch, false));
+    return bg_ws_bytes(bg_plan((rows + 15) / 16, cols, batch, false, device_cus()));
 }
 
 int sli_matmul_batch(const float* x, const void* w, int w_dtype, float* y, int32_t rows, int32_t cols, int32_t batch,
@@ -263,7 +263,7 @@ int sli_matmul_batch(const float* x, const void* w, int w_dtype, float* y, int32
     SLI_CHECK(rows > 0 && cols > 0 && cols % 32 == 0, SLI_ERR_SHAPE, "sli_matmul_batch: cols must be a multiple of 32");
     SLI_CHECK(batch >= 1 && batch <= kBgMaxBatch, SLI_ERR_SHAPE, "sli_matmul_batch: batch must be in [1, 8]");
     SLI_CHECK((uintptr_t)x % 16 == 0 && (uintptr_t)w % 16 == 0, SLI_ERR_ARG, "sli_matmul_batch: 16-byte alignment");
-    const BgPlan p = bg_plan((rows + 15) / 16, cols, batch, false);
+    const BgPlan p = bg_plan((rows + 15) / 16, cols, batch, false, device_cus());
     SLI_CHECK(p.groups > 0, SLI_ERR_SHAPE, "sli_matmul_batch: no tiling fits");
     SLI_CHECK(workspace_bytes >= bg_ws_bytes(p), SLI_ERR_ARG, "sli_matmul_batch: workspace too small");
     hipStream_t s = as_stream(stream);

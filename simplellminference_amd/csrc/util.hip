@@ -1,4 +1,5 @@
 // util.hip — C-ABI error plumbing and device-memory helpers (include/sli.h "device helpers").
+#include <atomic>
 #include <cstdio>
 #include <string>
 
@@ -18,6 +19,17 @@ int fail(int code, const std::string& msg) {
 int hip_fail(hipError_t e, const char* what) {
     g_last_error = std::string(what) + ": " + hipGetErrorString(e);
     return e == hipErrorOutOfMemory ? SLI_ERR_NOMEM : SLI_ERR_HIP;
+}
+
+int device_cus() {
+    static std::atomic<int> cache[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    int n = cache[dev].load(std::memory_order_relaxed);
+    if (n > 0) return n;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev].store(n, std::memory_order_relaxed);
+    return n;
 }
 
 }  // namespace sli

@@ -40,6 +40,9 @@ PRESETS = {
     # BASELINE.json configs[0]: tiny-llama shape (2 layers, d=256, 4 heads), greedy 32 tokens
     "tiny": LlamaModelConfig(512, 64, 256, 256, 768, 64, 2, 4, 4, 1e-5, 10000.0),
     "tiny-gqa": LlamaModelConfig(512, 64, 256, 128, 768, 64, 2, 4, 2, 1e-5, 10000.0),
+    # tiny shapes wide enough for tensor parallelism over 8 ranks (heads and kv heads divisible by 8)
+    "tiny-h8": LlamaModelConfig(512, 64, 512, 512, 1024, 64, 2, 8, 8, 1e-5, 10000.0),
+    "tiny-gqa-h16": LlamaModelConfig(512, 64, 1024, 512, 2048, 64, 2, 16, 8, 1e-5, 10000.0),
     # configs[1..3]: Llama-2 7B (public model card shape), ctx 2048
     "llama2-7b": LlamaModelConfig(32000, 128, 4096, 4096, 11008, 2048, 32, 32, 32, 1e-5, 10000.0),
     # configs[4]: Llama-3 8B (GQA), ctx 4096
@@ -74,18 +77,24 @@ class LlamaModel:
         self._h = None
 
     # ------------------------------------------------------------------ model.h:63-67
-    def init(self) -> "LlamaModel":
+    def _config_struct(self) -> ModelConfig:
         c = self.config
         if c.kv_hidden_size != c.num_key_value_heads * c.head_dim:
             raise ValueError("kv_hidden_size must equal num_key_value_heads * head_dim")
-        mc = ModelConfig(c.vocab_size, c.hidden_size, c.num_attention_heads, c.num_key_value_heads, c.head_dim,
-                         c.intermediate_size, c.num_hidden_layers, c.max_length, c.rms_norm_eps, c.rope_theta,
-                         self.w_dtype, self.kv_dtype, self.act_mode, self.tp_rank, self.tp_size, self.device,
-                         self.batch)
+        return ModelConfig(c.vocab_size, c.hidden_size, c.num_attention_heads, c.num_key_value_heads, c.head_dim,
+                           c.intermediate_size, c.num_hidden_layers, c.max_length, c.rms_norm_eps, c.rope_theta,
+                           self.w_dtype, self.kv_dtype, self.act_mode, self.tp_rank, self.tp_size, self.device,
+                           self.batch)
+
+    def init(self) -> "LlamaModel":
+        mc = self._config_struct()
         h = ctypes.c_void_p()
         cid = ctypes.create_string_buffer(self.comm_id, len(self.comm_id)) if self.comm_id else None
         call("sli_model_create", ctypes.byref(mc), cid, ctypes.byref(h))
         self._h = h
+        return self._load_weights()
+
+    def _load_weights(self) -> "LlamaModel":
         if self.model_path:
             call("sli_model_load_flat", self._h, self.model_path.encode())
         elif self.seed is not None:
@@ -94,10 +103,12 @@ class LlamaModel:
             raise ValueError("No model weigth file!")  # model.cpp:205-207
         return self
 
+    _borrowed = False  # a rank of a TPGroup: the group owns (steps, destroys) the engine
+
     def close(self):
-        if self._h is not None:
+        if self._h is not None and not self._borrowed:
             _lib.load().sli_model_destroy(self._h)
-            self._h = None
+        self._h = None
 
     def __del__(self):
         try:
@@ -230,6 +241,16 @@ class LlamaModel:
         call("sli_model_step_bytes", self._h, ctypes.byref(w), ctypes.byref(k))
         return w.value, k.value
 
+    FAMILIES = ("qkv", "attention", "wo", "gate_up", "down", "lm_head")
+
+    def time_families(self, iters: int = 20) -> dict:
+        """Per kernel family: mean device µs per launch, algorithmic bytes per launch, launches per step."""
+        n = len(self.FAMILIES)
+        us, b, k = (ctypes.c_double * n)(), (ctypes.c_double * n)(), (ctypes.c_int32 * n)()
+        call("sli_model_time_families", self._h, iters, us, b, k)
+        return {f: {"avg_us": us[i], "bytes_per_launch": b[i], "launches_per_step": k[i]}
+                for i, f in enumerate(self.FAMILIES)}
+
     def time_gemv(self, iters: int = 20) -> dict:
         us, b, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int32()
         call("sli_model_time_gemv", self._h, iters, ctypes.byref(us), ctypes.byref(b), ctypes.byref(n))
@@ -242,3 +263,94 @@ def comm_id() -> bytes:
     buf = ctypes.create_string_buffer(n)
     call("sli_comm_get_id", buf)
     return buf.raw
+
+
+class TPGroup:
+    """In-process tensor parallelism (sli_tp_group): ``tp_size`` rank engines on one
+    device, stepped in lockstep by one graph whose all-reduces are device-side reductions over the ranks'
+    buffers. ``ranks[r]`` is a borrowed ``LlamaModel`` of rank r (weights, state, logits shard)."""
+
+    def __init__(self, config: LlamaModelConfig, tp_size: int, w_dtype: str = "f16", kv_dtype: str = "f16",
+                 act_mode: int = 0, device: int = 0, seed: int | None = None, batch: int = 1,
+                 model_path: str = ""):
+        self.config, self.tp_size, self.batch = config, tp_size, batch
+        proto = LlamaModel(model_path=model_path, config=config, w_dtype=w_dtype, kv_dtype=kv_dtype,
+                           act_mode=act_mode, tp_rank=0, tp_size=tp_size, device=device, seed=seed, batch=batch)
+        mc = proto._config_struct()
+        g = ctypes.c_void_p()
+        call("sli_tp_group_create", ctypes.byref(mc), tp_size, ctypes.byref(g))
+        self._g = g
+        self.ranks = []
+        for r in range(tp_size):
+            h = ctypes.c_void_p()
+            call("sli_tp_group_rank", g, r, ctypes.byref(h))
+            m = LlamaModel(model_path=model_path, config=config, w_dtype=w_dtype, kv_dtype=kv_dtype,
+                           act_mode=act_mode, tp_rank=r, tp_size=tp_size, device=device, seed=seed, batch=batch)
+            m._h = h
+            m._borrowed = True
+            self.ranks.append(m)
+
+    def init(self) -> "TPGroup":
+        for m in self.ranks:
+            m._load_weights()
+        return self
+
+    def close(self):
+        if self._g is not None:
+            for m in self.ranks:
+                m._h = None
+            _lib.load().sli_tp_group_destroy(self._g)
+            self._g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def fill_kv_synthetic(self, seed: int, upto: int):
+        for m in self.ranks:
+            m.fill_kv_synthetic(seed, upto)
+
+    def step(self):
+        call("sli_tp_group_step", self._g)
+
+    def sync(self):
+        call("sli_tp_group_sync", self._g)
+
+    def logits(self) -> np.ndarray:
+        """The full-vocabulary logits of the last step ([vocab] or [batch, vocab]), the ranks' shards in place."""
+        parts = [m.logits()[0] for m in self.ranks]
+        return np.concatenate(parts, axis=-1)
+
+    def forward_batch(self, tokens, positions) -> np.ndarray:
+        for m in self.ranks:
+            for b in range(self.batch):
+                m.set_state_seq(b, int(tokens[b]), int(positions[b]), advance=False)
+        self.step()
+        return self.logits().reshape(self.batch, -1)
+
+    def forward(self, token: int, pos: int) -> np.ndarray:
+        return self.forward_batch([token] * self.batch, [pos] * self.batch)[0]
+
+    def predict_batch(self, prompts, max_length: int, want_logits: bool = False):
+        if len(prompts) != self.batch:
+            raise ValueError(f"need {self.batch} prompts")
+        ld = max(len(p) for p in prompts)
+        P = np.zeros((self.batch, ld), np.int32)
+        for b, p in enumerate(prompts):
+            P[b, :len(p)] = p
+        lens = np.array([len(p) for p in prompts], np.int32)
+        toks = np.empty((self.batch, max_length), np.int32)
+        V = self.config.vocab_size
+        logits = np.empty((max_length, self.batch, V), np.float32) if want_logits else None
+        call("sli_tp_group_predict_batch", self._g, P.ctypes.data_as(ctypes.c_void_p),
+             lens.ctypes.data_as(ctypes.c_void_p), ld, max_length, toks.ctypes.data_as(ctypes.c_void_p),
+             logits.ctypes.data_as(ctypes.c_void_p) if want_logits else None)
+        return (toks, logits.transpose(1, 0, 2).copy()) if want_logits else toks
+
+    def predict(self, prompt_ids, max_length: int, want_logits: bool = False):
+        r = self.predict_batch([list(prompt_ids)] * self.batch, max_length, want_logits)
+        if want_logits:
+            return r[0][0], r[1][0]
+        return r[0]

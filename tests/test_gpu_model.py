@@ -106,3 +106,15 @@ def test_llama7b_full_properties(gpu):
     wb, kb = gm.step_bytes()
     assert abs(wb - 13.214e9) / 13.214e9 < 0.01 and abs(kb - 1.074e9) / 1.074e9 < 0.01
     gm.close()
+
+
+def test_short_context_many_heads(gpu, oracle):
+    """Llama-2-7B heads (32 x 128, fused QKV rows 12288) with max_length 64: the QKV epilogue's entry
+    prefetch must stay inside the [T][hd/2] RoPE table (64 x 64 floats < 12288 rows)."""
+    om, gm = _models(oracle, "llama2-7b", "f16", "f16", seed=2, num_hidden_layers=2, max_length=64)
+    otok, olog = om.predict(PROMPT, 8)
+    gtok, glog = gm.predict(PROMPT, 8, want_logits=True)
+    assert np.array_equal(gtok, otok)
+    assert np.abs(glog - olog).max() <= 1e-3
+    gm.close()
+    om.close()

@@ -182,3 +182,32 @@ def test_argmax_first_max(gpu, oracle):
     x = np.full(64, -np.inf, np.float32)
     x[40] = -1e30
     assert int(ops.argmax(_t(torch, x)).item()) == 40
+
+
+NAN = np.float32("nan")
+SPECIAL = [
+    [-0.0, 0.0],                      # -0 == +0 under `<`: the first one wins
+    [0.0, -0.0],
+    [-1.0, -0.0, 0.0, -0.0],
+    [NAN, 1.0, 5.0],                  # NaN at index 0 is never displaced
+    [1.0, NAN, 5.0, NAN],             # a NaN later never displaces the best
+    [-np.inf, NAN, -np.inf],
+    [NAN, NAN],
+    [3.0, NAN, 3.0, np.inf, NAN, np.inf],
+]
+
+
+@pytest.mark.parametrize("vals", SPECIAL, ids=[str(i) for i in range(len(SPECIAL))])
+def test_argmax_signed_zero_and_nan(gpu, oracle, vals):
+    """std::max_element's `<` scan (argmax.cpp:11) on the values `<` does not order: bit-exact index."""
+    torch = gpu
+    from simplellminference_amd import ops
+    x = np.array(vals, np.float32)
+    want = oracle.argmax(x)
+    assert int(ops.argmax(_t(torch, x)).item()) == want
+    # the same values inside a long row (the LM-head shape): shifted right, padded with -inf
+    y = np.full(32000, -np.inf, np.float32)
+    y[1000:1000 + x.size] = x
+    if x.size and np.isnan(x[0]):
+        y[1000] = -np.inf  # a NaN away from index 0 loses: the oracle says the same
+    assert int(ops.argmax(_t(torch, y)).item()) == oracle.argmax(y)

@@ -163,3 +163,22 @@ def test_reference_edge_cases(oracle):
     assert np.array_equal(q2[:128], k2)
     # swiglu is the reference variant sigmoid(gate)*up, not SiLU
     assert np.isclose(oracle.swiglu(np.array([2.0], np.float32), np.array([0.0], np.float32))[0], 1.0)
+
+
+def _max_element(x):
+    """std::max_element (argmax.cpp:11) restated: keep the best unless `best < x[i]`."""
+    best = 0
+    for i in range(1, len(x)):
+        if x[best] < x[i]:
+            best = i
+    return best
+
+
+def test_argmax_special_values_follow_max_element(oracle):
+    """The oracle's argmax on ±0 and NaN is std::max_element's `<` scan (the GPU key must match it)."""
+    nan = np.float32("nan")
+    cases = [[-0.0, 0.0], [0.0, -0.0], [nan, 1.0, 5.0], [1.0, nan, 5.0, nan], [-np.inf, nan, -np.inf],
+             [nan, nan], [3.0, nan, 3.0, np.inf, nan, np.inf]]
+    for c in cases:
+        x = np.array(c, np.float32)
+        assert oracle.argmax(x) == _max_element(x), c

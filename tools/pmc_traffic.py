@@ -41,5 +41,27 @@ res[key] = {
     "per_kernel_mean_kib_raw": {k.split("(")[0][:90]: round(sum(v) / len(v), 1) for k, v in per.items()
                                 if weight_kernel(k)},
 }
+
+
+def family(k):
+    """Kernel family of a decode-step dispatch (the names bench.py's roofline uses), or None."""
+    if "attn_partial_kernel" in k:
+        return "attention"
+    for tag, fam in (("EpiQKV", "qkv"), ("EpiSwiGLU", "gate_up"), ("EpiLogits", "lm_head")):
+        if tag in k and weight_kernel(k):
+            return fam
+    if "gemv_kernel" in k and "EpiStore<1>" in k:  # wo streams U = 2 vectors per lane, down U = 6
+        return "wo" if ", 1, 2, true" in k else "down" if ", 1, 6, true" in k else None
+    if "bgemm_kernel" in k and "BgEpiStore" in k:
+        return "wo+down"  # one instantiation serves both batched row-parallel projections
+    return None
+
+
+fam = defaultdict(list)
+for k, vs in per.items():
+    f = family(k)
+    if f:
+        fam[f] += vs
+res[key]["per_family_hbm_bytes_per_launch"] = {f: round(2 * 1024 * sum(v) / len(v)) for f, v in fam.items()}
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res[key], indent=1))
