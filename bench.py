@@ -13,10 +13,15 @@ architecture (no checkpoints are reachable); every input is resident in HBM befo
 Under TP each rank holds 1/N of the heads / FFN columns / vocab and the step all-reduces twice per
 layer over RCCL; value = tokens/s of the whole job (1 token per step across all ranks).
 
-Rank 0 prints one JSON line. `roofline` prices the dominant kernel family (the weight-streaming GEMVs,
-92.5 % of the step's bytes): algorithmic bytes per launch / mean launch time measured with HIP events
-on the engine's stream. `cpu_baseline` times the C oracle (single-threaded restatement of the
-reference CPU path) on a bounded sample and projects the full model's tokens/s.
+Rank 0 prints one JSON line. `roofline` prices the DOMINANT kernel (the family with the largest share
+of the step's device time, e.g. the fused RMSNorm + gate/up GEMV + SwiGLU at C1): its algorithmic bytes
+per launch / its mean launch time, measured live with HIP events on the engine's own stream
+(sli_model_time_families); `roofline.families` lists every family the same way, and `roofline.traffic`
+is that kernel's HBM bytes per launch from the committed rocprofv3 FETCH_SIZE pass (x2 gfx950
+correction). `greedy_64` is a true 64-token greedy decode (positions ctx-64 .. ctx-1, the state advancing
+on the device) beside the idempotent-step timing. `cpu_baseline` times the C oracle (single-threaded
+restatement of the reference CPU path) pinned to one host core, on a bounded sample, and projects the
+full model's tokens/s.
 """
 from __future__ import annotations
 
@@ -33,6 +38,18 @@ sys.path.insert(0, ROOT)
 METRIC = "decode tokens/sec, Llama-7B fp16 seq=1 ctx=2048, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 CTX = 2048
+FAMILY_KERNELS = {
+    False: {"step": "ps_step_kernel (the whole decode step as one persistent launch: 5 phases x 32 layers + LM head)",
+            "qkv": "gemv_kernel<EpiQKV> (RMSNorm + [wq;wk;wv] GEMV + RoPE + K/V write)",
+            "attention": "attn_partial_kernel (split-context flash decode + last-arriver merge)",
+            "wo": "gemv_kernel<EpiStore, U=2> (wo GEMV + residual add)",
+            "gate_up": "gemv_kernel<EpiSwiGLU> (RMSNorm + [gate;up] GEMV + sigmoid(g)*u)",
+            "down": "gemv_kernel<EpiStore, U=6> (down GEMV + residual add)",
+            "lm_head": "gemv_kernel<EpiLogits> (RMSNorm + tied LM head + argmax keys)"},
+    True: {"qkv": "bgemm_kernel<BgEpiQKV> (MFMA 16x16x32 f16)", "attention": "attn_partial_kernel (batched kv heads)",
+           "wo": "bgemm_kernel<BgEpiStore> (MFMA)", "gate_up": "bgemm_kernel<BgEpiSwiGLU> (MFMA)",
+           "down": "bgemm_kernel<BgEpiStore> (MFMA)", "lm_head": "bgemm_kernel<BgEpiLogits> (MFMA)"},
+}
 
 
 def parse():
@@ -44,6 +61,9 @@ def parse():
     ap.add_argument("--preset", default="llama2-7b")
     ap.add_argument("--ctx", type=int, default=CTX)
     ap.add_argument("--batch", type=int, default=1, help="sequences decoding in lockstep (MFMA projections if > 1)")
+    ap.add_argument("--exec", default="launches", choices=["launches", "persistent"],
+                    help="launches: one graph of fused launches (default, fastest measured); persistent: the whole "
+                         "step as one launch (batch 1, TP 1; DESIGN.md §4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample budget")
     ap.add_argument("--gemv-iters", type=int, default=20)
@@ -60,6 +80,10 @@ def cpu_baseline(budget_s: float, preset_name: str = "llama2-7b", ctx: int = CTX
     cfg = O.Config(pc.vocab_size, pc.hidden_size, pc.num_attention_heads, pc.num_key_value_heads, pc.head_dim,
                    pc.intermediate_size, 2, ctx, pc.rms_norm_eps, pc.rope_theta)
     n_layers = pc.num_hidden_layers
+    # pinned to one host core in-process (no re-exec): the reference CPU path is single-threaded
+    prev = os.sched_getaffinity(0)
+    core = max(prev)
+    os.sched_setaffinity(0, {core})
     m = O.Model(cfg, seed=1, wmode=O.W_F32)
     m.fill_kv_synthetic(7, ctx - 1)
     t_lay, t_head, t_emb = [], [], []
@@ -73,13 +97,17 @@ def cpu_baseline(budget_s: float, preset_name: str = "llama2-7b", ctx: int = CTX
         if time.perf_counter() - t0 >= budget_s or len(t_lay) >= 50:
             break
     m.close()
+    os.sched_setaffinity(0, prev)
     layer, head, emb = statistics.median(t_lay), statistics.median(t_head), statistics.median(t_emb)
     step = emb + n_layers * layer + head
-    return {"value": 1.0 / step, "unit": "tokens/s", "cores": 1, "kind": "port",
-            "sample": (f"C oracle (oracle/sli_oracle.c, fp32, 1 thread, one sequence per step as the reference) on "
-                       f"{len(t_lay)} decode steps of a 2-layer {preset_name}-shape model (+{pc.vocab_size}x"
-                       f"{pc.hidden_size} tied head) at pos {ctx - 1}; median layer {layer * 1e3:.1f} ms, head "
-                       f"{head * 1e3:.1f} ms; full {n_layers}-layer step projected {step:.2f} s")}
+    sample_step = emb + 2 * layer + head
+    return {"value": 1.0 / step, "unit": "tokens/s", "cores": 1, "core_id": core, "kind": "port",
+            "sample_step_s": round(sample_step, 4),
+            "sample": (f"C oracle (oracle/sli_oracle.c, fp32, 1 thread pinned to core {core}, one sequence per "
+                       f"step as the reference) on {len(t_lay)} decode steps of a 2-layer {preset_name}-shape model "
+                       f"(+{pc.vocab_size}x{pc.hidden_size} tied head) at pos {ctx - 1}: median {sample_step:.3f} s per "
+                       f"sample step (layer {layer * 1e3:.1f} ms, head {head * 1e3:.1f} ms); full {n_layers}-layer step "
+                       f"projected {step:.2f} s = embed + {n_layers} x layer + head")}
 
 
 def main():
@@ -110,6 +138,8 @@ def main():
     B = a.batch
     model = LlamaModel(config=cfg, w_dtype=a.w_dtype, kv_dtype="f16", tp_rank=rank, tp_size=world, comm_id=cid,
                        device=local, seed=1, batch=B).init()
+    exec_mode = a.exec
+    model.set_exec(exec_mode)
     model.fill_kv_synthetic(7, a.ctx - 1)
     for b in range(B):  # every sequence at position ctx-1 (KV rows 0..ctx-2 resident), its own token
         model.set_state_seq(b, 1234 + 17 * b, a.ctx - 1, advance=False)
@@ -137,16 +167,44 @@ def main():
     if st["error"]:
         raise SystemExit(f"device error flag {st['error']}")
     wbytes, kvbytes = model.step_bytes()
+    fam = model.time_families(a.gemv_iters)
     g = model.time_gemv(a.gemv_iters)
-    achieved = g["bytes_per_launch"] / (g["avg_us"] * 1e-6) / 1e9
+    if exec_mode == "persistent":
+        # the step IS one kernel (ps_step_kernel): its algorithmic bytes (all weights + the live K/V) per launch
+        dom = "step"
+        d = {"avg_us": model.time_steps(a.gemv_iters), "bytes_per_launch": wbytes + kvbytes, "launches_per_step": 1}
+        step_dev_us = d["avg_us"]
+    else:
+        # the dominant kernel: the family with the largest device time per step
+        dom = max(fam, key=lambda f: fam[f]["avg_us"] * fam[f]["launches_per_step"])
+        d = fam[dom]
+        step_dev_us = sum(f["avg_us"] * f["launches_per_step"] for f in fam.values())
+    achieved = d["bytes_per_launch"] / (d["avg_us"] * 1e-6) / 1e9
 
-    traffic = None
+    # a true greedy decode beside the idempotent-step timing: 64 tokens at positions ctx-64 .. ctx-1, the
+    # state (position, next token = greedy argmax) advancing on the device every step
+    g_steps = min(64, a.ctx - 1)
+    for b in range(B):
+        model.set_state_seq(b, 1234 + 17 * b, a.ctx - 1 - g_steps, advance=True)
+    barrier()
+    tg = time.perf_counter()
+    for _ in range(g_steps):
+        model.step()
+    barrier()
+    tg = time.perf_counter() - tg
+    gst = [model.state(b) for b in range(B)]
+    greedy = {"tokens": B * g_steps, "tokens_per_s": round(B * g_steps / tg, 2), "ms_per_step": round(1e3 * tg / g_steps, 4),
+              "positions": f"{a.ctx - 1 - g_steps}..{a.ctx - 2}",
+              "final_pos_ok": all(x["pos"] == a.ctx - 1 for x in gst) and not any(x["error"] for x in gst)}
+
+    traffic, traffic_family = None, {}
     if os.path.exists(a.traffic_json):
         try:
             tj = json.load(open(a.traffic_json))
             key = f"{a.preset}/{a.w_dtype}/tp{world}" + (f"/b{B}" if B > 1 else "")
             if key in tj:
-                traffic = tj[key]["hbm_bytes_per_launch"]
+                traffic_family = tj[key].get("per_family_hbm_bytes_per_launch", {})
+                traffic = traffic_family.get(dom)
         except (OSError, ValueError, KeyError):
             traffic = None
 
@@ -168,19 +226,41 @@ def main():
         "config": {"workload": f"{a.preset} decode step, batch {B}, ctx {a.ctx}, tensor parallel {world}",
                    "global_batch": B, "seq_len": a.ctx, "parallelism": f"tp{world}", "weights": a.w_dtype,
                    "kv_cache": "fp16", "accumulate": "fp32",
-                   "step_bytes_per_gpu": round(wbytes + kvbytes), "hbm_roofline_tokens_per_s":
-                       round(HBM_PEAK_GBS * 1e9 / (wbytes + kvbytes), 1),
+                   "step_bytes_per_gpu": round(wbytes + kvbytes),
+                   "hbm_roofline_tokens_per_s": round(B * HBM_PEAK_GBS * 1e9 / (wbytes + kvbytes), 1),
                    "step_frac_of_hbm_peak": round((wbytes + kvbytes) / (ms * 1e-3) / (HBM_PEAK_GBS * 1e9), 4)},
-        "roofline": {"bound": "hbm", "kernel": ("gemv_kernel (qkv/wo/gate-up/down/lm-head weight streaming)" if B == 1
-                                                else "bgemm_kernel (MFMA 16x16x32 f16, qkv/wo/gate-up/down/lm-head)"),
+        "exec": exec_mode,
+        "roofline": {"bound": "hbm", "kernel": f"{dom}: {FAMILY_KERNELS[B > 1][dom]}",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "avg_launch_us": round(g["avg_us"], 3), "algorithmic_bytes_per_launch": round(g["bytes_per_launch"]),
-                     "launches_per_step": g["launches_per_step"]},
+                     "avg_launch_us": round(d["avg_us"], 3), "algorithmic_bytes_per_launch": round(d["bytes_per_launch"]),
+                     "launches_per_step": d["launches_per_step"],
+                     "share_of_step_device_time": round(d["avg_us"] * d["launches_per_step"] / step_dev_us, 4),
+                     "families_note": ("per-family timing of the launch path's kernels (the same arithmetic; "
+                                       "the persistent step runs them as phases of one launch)"
+                                       if exec_mode == "persistent" else "the step's launches by family"),
+                     "families": {f: {"avg_launch_us": round(v["avg_us"], 3),
+                                      "bytes_per_launch": round(v["bytes_per_launch"]),
+                                      "launches_per_step": v["launches_per_step"],
+                                      "gbs": round(v["bytes_per_launch"] / (v["avg_us"] * 1e-6) / 1e9, 1),
+                                      "frac": round(v["bytes_per_launch"] / (v["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                                      "traffic": traffic_family.get(f)}
+                                  for f, v in fam.items()},
+                     "weight_streaming_average": {"avg_launch_us": round(g["avg_us"], 3),
+                                                  "bytes_per_launch": round(g["bytes_per_launch"]),
+                                                  "launches_per_step": g["launches_per_step"],
+                                                  "frac": round(g["bytes_per_launch"] / (g["avg_us"] * 1e-6) / 1e9
+                                                                / HBM_PEAK_GBS, 4)}},
+        "greedy_64": greedy,
     }
-    if B > 1:  # MFMA work of the dominant kernel family: 2 flop per weight per sequence
-        tflops = 2.0 * B * (g["bytes_per_launch"] / 2.0) / (g["avg_us"] * 1e-6) / 1e12
-        out["roofline"]["mfma"] = {"achieved_tflops": round(tflops, 2), "peak_tflops": 2500.0,
+    if B > 1:  # MFMA work of the batched projections: 2 flop per weight per sequence
+        wb_el = {"f16": 2.0, "i8": 1.0, "f32": 4.0}[a.w_dtype]
+        proj = [f for f in fam if f != "attention"]
+        flops = sum(2.0 * B * fam[f]["bytes_per_launch"] / wb_el * fam[f]["launches_per_step"] for f in proj)
+        t = sum(fam[f]["avg_us"] * fam[f]["launches_per_step"] for f in proj) * 1e-6
+        tflops = flops / t / 1e12
+        out["roofline"]["mfma"] = {"kernel": "bgemm_kernel (v_mfma_f32_16x16x32_f16), all projections",
+                                   "achieved_tflops": round(tflops, 2), "peak_tflops": 2500.0,
                                    "frac": round(tflops / 2500.0, 5)}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a.cpu_seconds, a.preset, a.ctx)

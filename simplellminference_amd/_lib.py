@@ -8,7 +8,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsli.so")
+# SLI_LIB_VARIANT=<name> loads libsli_<name>.so from the same directory (A/B experiments in tools/ only)
+LIB_PATH = os.path.join(_HERE, "libsli.so" if not os.environ.get("SLI_LIB_VARIANT")
+                        else f"libsli_{os.environ['SLI_LIB_VARIANT']}.so")
 
 SLI_OK = 0
 STATUS = {0: "ok", 1: "invalid argument", 2: "shape mismatch", 3: "index out of range", 4: "HIP runtime error",
@@ -86,6 +88,8 @@ _SIGS = {
     "sli_model_set_prompt_seq": (c_int, [c_vp, c_i32, c_vp, c_i32]),
     "sli_model_get_state_seq": (c_int, [c_vp, c_i32, P_i32, P_i32, P_i32, P_i32]),
     "sli_model_get_history": (c_int, [c_vp, c_i32, c_i32, c_vp]),
+    "sli_model_set_exec": (c_int, [c_vp, c_i32]),
+    "sli_model_get_exec": (c_int, [c_vp, P_i32]),
     "sli_model_step": (c_int, [c_vp]),
     "sli_model_sync": (c_int, [c_vp]),
     "sli_model_get_logits": (c_int, [c_vp, c_vp, c_i32, P_i32]),
@@ -97,6 +101,8 @@ _SIGS = {
     "sli_model_stream": (c_int, [c_vp, ctypes.POINTER(c_vp)]),
     "sli_model_step_bytes": (c_int, [c_vp, P_d, P_d]),
     "sli_model_time_gemv": (c_int, [c_vp, c_i32, P_d, P_d, P_i32]),
+    "sli_model_ps_stamps": (c_int, [c_vp, c_vp, c_i64, P_i32]),
+    "sli_model_time_steps": (c_int, [c_vp, c_i32, P_d]),
     "sli_model_time_families": (c_int, [c_vp, c_i32, P_d, P_d, P_i32]),
     "sli_tp_group_create": (c_int, [ctypes.POINTER(ModelConfig), c_i32, ctypes.POINTER(c_vp)]),
     "sli_tp_group_destroy": (c_int, [c_vp]),

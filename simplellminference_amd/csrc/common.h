@@ -81,6 +81,9 @@ struct Vec16<float> {
         o[2] = __uint_as_float(v.z);
         o[3] = __uint_as_float(v.w);
     }
+    __device__ __forceinline__ static u32x4 pack(const float* f) {
+        return u32x4{__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]), __float_as_uint(f[3])};
+    }
 };
 template <>
 struct Vec16<__half> {
@@ -94,6 +97,16 @@ struct Vec16<__half> {
             o[2 * i] = f.x;
             o[2 * i + 1] = f.y;
         }
+    }
+    // inverse of unpack for values already representable in fp16 (exact)
+    __device__ __forceinline__ static u32x4 pack(const float* f) {
+        unsigned w[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const __half2 h = __floats2half2_rn(f[2 * i], f[2 * i + 1]);
+            w[i] = *reinterpret_cast<const unsigned*>(&h);
+        }
+        return u32x4{w[0], w[1], w[2], w[3]};
     }
 };
 template <>

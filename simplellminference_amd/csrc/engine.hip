@@ -29,6 +29,7 @@
 #include "common.h"
 #include "gemv.h"
 #include "ops_internal.h"
+#include "persist.h"
 #include "rope_table.h"
 #include "step_state.h"
 
@@ -84,6 +85,13 @@ struct sli_model {
     unsigned* bg_cnt = nullptr;           // their arrival counters (zero between launches)
     unsigned long long* bkeys = nullptr;  // [B] per-sequence argmax keys (all-reduced MAX under TP)
     int key_ld = 0;                       // per-sequence stride of the per-workgroup argmax keys
+    // SLI_EXEC_PERSISTENT (persist.h): the whole step as one launch
+    int exec = SLI_EXEC_LAUNCHES;
+    sli::PsArgs* ps_args = nullptr;  // device copy of the args record
+    unsigned* ps_sync = nullptr;     // barrier + merge counters, zeroed by a memset node before each launch
+    size_t ps_sync_bytes = 0;
+    size_t ps_lds = 0;
+    int ps_grid = 0;
 };
 
 // In-process tensor parallelism (the "fake communicator"): tp_size rank models on
@@ -114,6 +122,93 @@ static int model_alloc(sli_model* m, void** p, size_t bytes) {
         int rc_ = (expr);               \
         if (rc_ != SLI_OK) return rc_;  \
     } while (0)
+
+// ---------------------------------------------------------------- persistent step (persist.h)
+static int ps_launch_model(sli_model* m, bool prepare) {
+    PsArgs a{};
+    a.hd = m->hd;
+    a.hq = m->hq;
+    a.hkv = m->hkv;
+    return ps_launch(a, m->ps_args, m->c.w_dtype, m->c.kv_dtype, m->ps_grid, m->ps_lds, m->stream, prepare);
+}
+
+// Allocate the hand-off buffers and the args record of the persistent step (once per model).
+static int ps_setup(sli_model* m) {
+    if (m->ps_args) return SLI_OK;
+    SLI_CHECK(m->B == 1, SLI_ERR_STATE, "persistent step: batch 1 only (batched decode runs the MFMA launches)");
+    SLI_CHECK(!m->partial && !m->group, SLI_ERR_STATE, "persistent step: tensor parallelism runs the launches");
+    const int g = m->hq / m->hkv;
+    SLI_CHECK(g == 1 || g == 2, SLI_ERR_STATE, "persistent step: heads per kv head must be 1 or 2");
+    const int L = m->L, D = m->D, hd = m->hd;
+    const int splits = ps_max_splits(m->c.kv_dtype, hd, m->T);
+    PsArgs a{};
+    int rc = SLI_OK;
+    auto A = [&](void** p, size_t bytes) {
+        if (rc == SLI_OK) rc = model_alloc(m, p, bytes);
+    };
+    m->ps_sync_bytes = (sizeof(unsigned) * (size_t)(kPsSyncHeads + L * m->hkv) + 15) & ~(size_t)15;
+    A((void**)&m->ps_sync, m->ps_sync_bytes);
+    A((void**)&a.xv, sizeof(float) * (size_t)(2 * L + 1) * D);
+    A((void**)&a.qv, sizeof(float) * (size_t)L * m->hq * hd);
+    A((void**)&a.kvn, sizeof(float) * (size_t)L * 2 * m->hkv * hd);
+    A((void**)&a.part, sizeof(float) * (size_t)L * m->hq * splits * (hd + kAttnPartPad));
+    A((void**)&a.attn, sizeof(float) * (size_t)L * m->hq * hd);
+    A((void**)&a.actv, sizeof(float) * (size_t)L * m->Il);
+    m->ps_grid = device_cus();
+    A((void**)&a.keys, sizeof(unsigned long long) * m->ps_grid);
+    PsLayer* layers = nullptr;
+    A((void**)&layers, sizeof(PsLayer) * L);
+    PsArgs* dev = nullptr;
+    A((void**)&dev, sizeof(PsArgs));
+    if (rc != SLI_OK) return rc;
+    std::vector<PsLayer> hl(L);
+    for (int l = 0; l < L; ++l) {
+        const LayerW& w = m->layers[l];
+        hl[l] = PsLayer{w.qkv, w.qkv_s, w.wo, w.wo_s, w.gu, w.gu_s, w.down, w.down_s};
+    }
+    a.layers = layers;
+    a.emb = m->emb;
+    a.emb_s = m->emb_s;
+    a.norms = m->norms;
+    a.kc = m->kc;
+    a.vc = m->vc;
+    a.sin_t = m->sin_t;
+    a.cos_t = m->cos_t;
+    a.st = m->st;
+    a.prompt = m->prompt;
+    a.hist = m->hist;
+    a.logits = m->logits;
+    a.sync = m->ps_sync;
+    a.D = D;
+    a.L = L;
+    a.T = m->T;
+    a.hd = hd;
+    a.hq = m->hq;
+    a.hkv = m->hkv;
+    a.Il = m->Il;
+    a.V = m->V;
+    a.v_lo = m->v_lo;
+    a.v_n = m->v_n;
+    a.max_splits = splits;
+    a.eps = m->c.eps;
+    a.scale = 1.0f / sqrtf((float)hd);  // mha_kernel.cpp:41
+    a.act_mode = m->c.act_mode;
+    SLI_HIP(hipMemcpy(layers, hl.data(), sizeof(PsLayer) * L, hipMemcpyHostToDevice));
+    SLI_HIP(hipMemcpy(dev, &a, sizeof(PsArgs), hipMemcpyHostToDevice));
+    SLI_HIP(hipMemset(m->ps_sync, 0, m->ps_sync_bytes));
+    // LDS: the staged input (the widest phase input), the per-unit results, the reduction scratch; at
+    // least kPsMinLds so that no two workgroups share a CU
+    const int max_cols = std::max(std::max(D, m->Il), m->hq * hd);
+    const int max_units = std::max(std::max((m->hq + 2 * m->hkv) * hd / 2, std::max(D, m->Il)), (m->v_n + 1) / 2);
+    const size_t need =
+        sizeof(float) * ((size_t)kGemvLdsHead + max_cols + 2 * ((size_t)max_units / m->ps_grid + 2) + D + 4);
+    m->ps_lds = std::max(kPsMinLds, (need + 255) & ~(size_t)255);
+    SLI_CHECK(m->ps_lds <= 160 * 1024, SLI_ERR_SHAPE, "persistent step: LDS image exceeds 160 KiB");
+    a.wslot = (int)(m->ps_lds / sizeof(float)) - ((D + 3) & ~3);
+    SLI_HIP(hipMemcpy(dev, &a, sizeof(PsArgs), hipMemcpyHostToDevice));
+    m->ps_args = dev;
+    return ps_launch_model(m, true);
+}
 
 #define SLI_NCCL(expr)                                                                          \
     do {                                                                                        \
@@ -567,6 +662,10 @@ struct StepRecorder {
 
     // one model and its own communicator (none, RCCL, or the debug modes)
     static int record(sli_model* m) {
+        if (m->exec == SLI_EXEC_PERSISTENT) {
+            SLI_HIP(hipMemsetAsync(m->ps_sync, 0, m->ps_sync_bytes, m->stream));
+            return ps_launch_model(m, false);
+        }
         for (int p = 0; p < 2 * m->L; ++p) {
             SLI_TRY(record_phase(m, p));
             SLI_TRY(allreduce_x(m));
@@ -1093,6 +1192,28 @@ int sli_model_get_history(sli_model* m, int32_t seq, int32_t n, int32_t* out) {
     return SLI_OK;
 }
 
+int sli_model_set_exec(sli_model* m, int32_t mode) {
+    SLI_CHECK(m, SLI_ERR_ARG, "null model");
+    SLI_CHECK(mode == SLI_EXEC_LAUNCHES || mode == SLI_EXEC_PERSISTENT, SLI_ERR_ARG, "unknown execution mode");
+    SLI_HIP(hipSetDevice(m->c.device));
+    if (mode == SLI_EXEC_PERSISTENT) SLI_TRY(ps_setup(m));
+    if (mode != m->exec) {  // re-capture the step graph on the next step
+        SLI_HIP(hipStreamSynchronize(m->stream));
+        if (m->graph_exec) (void)hipGraphExecDestroy(m->graph_exec);
+        if (m->graph) (void)hipGraphDestroy(m->graph);
+        m->graph_exec = nullptr;
+        m->graph = nullptr;
+        m->exec = mode;
+    }
+    return SLI_OK;
+}
+
+int sli_model_get_exec(sli_model* m, int32_t* mode) {
+    SLI_CHECK(m && mode, SLI_ERR_ARG, "null argument");
+    *mode = m->exec;
+    return SLI_OK;
+}
+
 int sli_model_step(sli_model* m) {
     SLI_CHECK(m, SLI_ERR_ARG, "null model");
     SLI_CHECK(!m->group, SLI_ERR_STATE, "a rank of an in-process tp group steps with its group (sli_tp_group_step)");
@@ -1240,6 +1361,60 @@ int sli_model_step_bytes(sli_model* m, double* weight_bytes, double* kv_bytes) {
     double ctx = 0.0;
     for (const DevState& d : h) ctx += d.pos + 1.0;
     if (kv_bytes) *kv_bytes = 2.0 * m->L * ctx * m->hkv * hd * (double)m->kvbytes;
+    return SLI_OK;
+}
+
+int sli_model_ps_stamps(sli_model* m, uint64_t* host, int64_t n, int32_t* grid) {
+    SLI_CHECK(m && host && grid, SLI_ERR_ARG, "null argument");
+    SLI_HIP(hipSetDevice(m->c.device));
+    SLI_TRY(ps_setup(m));
+    const int64_t want = (int64_t)(2 + 5 * m->L) * m->ps_grid * 5;
+    *grid = m->ps_grid;
+    SLI_CHECK(n == want, SLI_ERR_SHAPE, "stamp buffer must hold (2 + 5L) * grid * 5 values");
+    struct Guard {
+        void* st = nullptr;
+        void* args = nullptr;
+        ~Guard() {
+            if (st) (void)hipFree(st);
+            if (args) (void)hipFree(args);
+        }
+    } g;
+    SLI_HIP(hipMalloc(&g.st, sizeof(uint64_t) * n));
+    SLI_HIP(hipMalloc(&g.args, sizeof(PsArgs)));
+    PsArgs a;
+    SLI_HIP(hipMemcpy(&a, m->ps_args, sizeof(PsArgs), hipMemcpyDeviceToHost));
+    a.stamps = (unsigned long long*)g.st;
+    SLI_HIP(hipMemcpy(g.args, &a, sizeof(PsArgs), hipMemcpyHostToDevice));
+    SLI_HIP(hipMemsetAsync(g.st, 0, sizeof(uint64_t) * n, m->stream));
+    SLI_HIP(hipMemsetAsync(m->ps_sync, 0, m->ps_sync_bytes, m->stream));
+    a.hd = m->hd;
+    SLI_TRY(ps_launch(a, (const PsArgs*)g.args, m->c.w_dtype, m->c.kv_dtype, m->ps_grid, m->ps_lds, m->stream, false));
+    SLI_HIP(hipStreamSynchronize(m->stream));
+    SLI_HIP(hipMemcpy(host, g.st, sizeof(uint64_t) * n, hipMemcpyDeviceToHost));
+    return SLI_OK;
+}
+
+int sli_model_time_steps(sli_model* m, int32_t iters, double* avg_us) {
+    SLI_CHECK(m && iters > 0 && avg_us, SLI_ERR_ARG, "bad argument");
+    SLI_CHECK(!m->group, SLI_ERR_STATE, "time a group through its own stream");
+    SLI_HIP(hipSetDevice(m->c.device));
+    struct Guard {
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        ~Guard() {
+            if (e0) (void)hipEventDestroy(e0);
+            if (e1) (void)hipEventDestroy(e1);
+        }
+    } g;
+    SLI_HIP(hipEventCreate(&g.e0));
+    SLI_HIP(hipEventCreate(&g.e1));
+    SLI_TRY(sli_model_step(m));  // captured and warm
+    SLI_HIP(hipEventRecord(g.e0, m->stream));
+    for (int i = 0; i < iters; ++i) SLI_HIP(hipGraphLaunch(m->graph_exec, m->stream));
+    SLI_HIP(hipEventRecord(g.e1, m->stream));
+    SLI_HIP(hipEventSynchronize(g.e1));
+    float ms = 0.0f;
+    SLI_HIP(hipEventElapsedTime(&ms, g.e0, g.e1));
+    *avg_us = 1000.0 * ms / iters;
     return SLI_OK;
 }
 

@@ -158,6 +158,19 @@ class LlamaModel:
         chunk = -(-c.vocab_size // self.tp_size)
         return max(0, min(chunk, c.vocab_size - self.tp_rank * chunk))
 
+    # ------------------------------------------------------------------ execution
+    EXEC = {"launches": 0, "persistent": 1}
+
+    def set_exec(self, mode: str) -> "LlamaModel":
+        """"launches" (one graph of fused launches) or "persistent" (the whole step as one launch)."""
+        call("sli_model_set_exec", self._h, self.EXEC[mode])
+        return self
+
+    def exec_mode(self) -> str:
+        v = ctypes.c_int32()
+        call("sli_model_get_exec", self._h, ctypes.byref(v))
+        return {i: k for k, i in self.EXEC.items()}[v.value]
+
     # ------------------------------------------------------------------ model.cpp:40-140
     def step(self):
         call("sli_model_step", self._h)
@@ -240,6 +253,12 @@ class LlamaModel:
         w, k = ctypes.c_double(), ctypes.c_double()
         call("sli_model_step_bytes", self._h, ctypes.byref(w), ctypes.byref(k))
         return w.value, k.value
+
+    def time_steps(self, iters: int = 20) -> float:
+        """Mean device µs of one replayed step (HIP events on the model's stream)."""
+        v = ctypes.c_double()
+        call("sli_model_time_steps", self._h, iters, ctypes.byref(v))
+        return v.value
 
     FAMILIES = ("qkv", "attention", "wo", "gate_up", "down", "lm_head")
 

@@ -368,3 +368,9 @@ int main(int argc, char** argv) {
     }
     return 0;
 }
+
+// the lab links without libsli: the persistent-grid size from the device (util.hip's device_cus)
+int sli::device_cus() {
+    int n = 0;
+    return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, 0) == hipSuccess && n > 0 ? n : 256;
+}
