@@ -64,6 +64,8 @@ def parse():
     ap.add_argument("--exec", default="launches", choices=["launches", "persistent"],
                     help="launches: one graph of fused launches (default, fastest measured); persistent: the whole "
                          "step as one launch (batch 1, TP 1; DESIGN.md §4)")
+    ap.add_argument("--prefill-tokens", type=int, default=512,
+                    help="after the decode timing: prefill a prompt of this many tokens (0: skip; batch 1 only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample budget")
     ap.add_argument("--gemv-iters", type=int, default=20)
@@ -262,6 +264,29 @@ def main():
         out["roofline"]["mfma"] = {"kernel": "bgemm_kernel (v_mfma_f32_16x16x32_f16), all projections",
                                    "achieved_tflops": round(tflops, 2), "peak_tflops": 2500.0,
                                    "frac": round(tflops / 2500.0, 5)}
+    if a.prefill_tokens > 1 and B == 1 and a.prefill_tokens <= a.ctx:
+        # prompt prefill: positions 0..n-2 eight at a time through the MFMA projections
+        n = a.prefill_tokens
+        ids = [(1 + 7919 * i) % cfg.vocab_size for i in range(n)]
+        model.prefill(ids)  # warm-up: capture + first run
+        barrier()
+        tp = time.perf_counter()
+        reps = 3
+        for _ in range(reps):
+            model.prefill(ids)
+        barrier()
+        tp = (time.perf_counter() - tp) / reps
+        wb_el = {"f16": 2.0, "i8": 1.0, "f32": 4.0}[a.w_dtype]
+        params = (wbytes - (4.0 * 0 if a.w_dtype != "i8" else 0.0)) / wb_el - cfg.vocab_size * cfg.hidden_size / world
+        steps = -(-(n - 1) // 8)
+        flops = 2.0 * params * 8 * steps  # every lane of every chunk, the padding lanes included
+        out["prefill"] = {"prompt_tokens": n, "positions_prefilled": n - 1, "chunk_steps": steps,
+                          "seconds": round(tp, 5), "tokens_per_s": round((n - 1) / tp, 1),
+                          "weight_bytes_streamed": round(steps * (wbytes - cfg.vocab_size * cfg.hidden_size * wb_el)),
+                          "mfma_tflops": round(flops / tp / 1e12, 2), "mfma_peak_tflops": 2500.0,
+                          "path": ("MFMA bgemm (v_mfma_f32_16x16x32_f16), 8 positions per step" if a.w_dtype == "f16"
+                                   and world == 1 else "decode step, teacher-forced (no MFMA path for this config)"),
+                          "vs_token_by_token_s": round((n - 1) * ms * 1e-3, 4)}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a.cpu_seconds, a.preset, a.ctx)
     model.close()

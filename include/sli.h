@@ -173,6 +173,16 @@ int sli_model_set_state_seq(sli_model* m, int32_t seq, int32_t token, int32_t po
 int sli_model_set_prompt_seq(sli_model* m, int32_t seq, const int32_t* ids, int32_t n);
 int sli_model_get_state_seq(sli_model* m, int32_t seq, int32_t* pos, int32_t* token, int32_t* last_argmax,
                             int32_t* error);
+/* Prompt prefill (batch-1 models): positions 0 .. n-2 of the prompt run through the layers kPfLanes = 8 at a
+ * time, the projections as an MFMA skinny GEMM over the positions (fp16 weights, no tensor parallelism;
+ * otherwise through the decode step, teacher-forced), filling the K/V cache; the state is left at
+ * (token ids[n-1], position n-1, advancing, prompt = ids), so the next sli_model_step yields the first
+ * greedy token exactly as the reference's token-by-token predict (model.cpp:157-165) would. */
+int sli_model_prefill(sli_model* m, const int32_t* ids, int32_t n);
+/* sli_model_predict with the prompt prefilled: tokens_out[t] as sli_model_predict; logits_out rows for
+ * positions < n_prompt - 1 (not computed by the prefill) are NaN. */
+int sli_model_predict_prefill(sli_model* m, const int32_t* prompt, int32_t n_prompt, int32_t max_length,
+                              int32_t* tokens_out, float* logits_out);
 /* The tokens fed at positions [0, n) of sequence seq. */
 int sli_model_get_history(sli_model* m, int32_t seq, int32_t n, int32_t* out);
 /* Execution of the step (the graph is re-captured on the next step after a change):

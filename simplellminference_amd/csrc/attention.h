@@ -34,6 +34,8 @@ struct AttnArgs {
     int seq_heads;          // kv heads per sequence: a batch is B sequences of seq_heads kv heads each
     int pos_seq_stride;     // int32s between consecutive sequences' positions at pos_dev
     unsigned long long* stamps = nullptr;  // diagnostic (tools/attn_lab): per-workgroup s_memrealtime x4
+    int cache_heads = 0;    // > 0: the cache holds cache_heads kv heads shared by every sequence (prefill lanes
+                            // of one sequence): kv head kvh reads cache head kvh % cache_heads
 };
 
 // Position of the sequence that owns (batched) kv head kvh.
@@ -95,8 +97,9 @@ __device__ __forceinline__ bool attn_publish(const AttnArgs<KT>& a, int kvh, int
         for (int e = 0; e < EPV; ++e) ov[g][e] = 0.0f;
     }
     if (live_wave) {
-        const KT* kb = a.k + (long long)kvh * a.head_stride + li * EPV;
-        const KT* vb = a.v + (long long)kvh * a.head_stride + li * EPV;
+        const int ch = a.cache_heads > 0 ? kvh % a.cache_heads : kvh;
+        const KT* kb = a.k + (long long)ch * a.head_stride + li * EPV;
+        const KT* vb = a.v + (long long)ch * a.head_stride + li * EPV;
         u32x4 kr[kAttnNit], vr[kAttnNit];
 #pragma unroll
         for (int it = 0; it < kAttnNit; ++it) {

@@ -400,6 +400,8 @@ struct BgEpiQKV {
     const float* sin_t;
     const float* cos_t;
     int hq, hkv, hd, T;
+    int kv_seq = 1;  // 1: sequence b owns cache heads [b*hkv, (b+1)*hkv); 0: one cache shared by every lane
+                     // (prefill lanes of one sequence at consecutive positions)
     __device__ int row(int t, int i) const {
         const int half = hd >> 1;
         const int u = t * 8 + (i & 7);
@@ -420,12 +422,12 @@ struct BgEpiQKV {
                 q[d] = r0;
                 q[d + half] = r1;
             } else {
-                KT* kp = kc + (((size_t)b * hkv + (uh - hq)) * T + pos) * hd;
+                KT* kp = kc + (((size_t)b * kv_seq * hkv + (uh - hq)) * T + pos) * hd;
                 kp[d] = from_f32<KT>(r0);
                 kp[d + half] = from_f32<KT>(r1);
             }
         } else {
-            KT* vp = vc + (((size_t)b * hkv + (uh - hq - hkv)) * T + pos) * hd;
+            KT* vp = vc + (((size_t)b * kv_seq * hkv + (uh - hq - hkv)) * T + pos) * hd;
             vp[d] = from_f32<KT>(a0);
             vp[d + half] = from_f32<KT>(a1);
         }

@@ -85,6 +85,18 @@ struct sli_model {
     unsigned* bg_cnt = nullptr;           // their arrival counters (zero between launches)
     unsigned long long* bkeys = nullptr;  // [B] per-sequence argmax keys (all-reduced MAX under TP)
     int key_ld = 0;                       // per-sequence stride of the per-workgroup argmax keys
+    // prompt prefill (sli_model_prefill): kPfLanes prompt positions of this one sequence per step, the
+    // projections on MFMA (bgemm.h), every lane writing its K/V row into the model's own cache
+    struct Prefill {
+        float *x = nullptr, *q = nullptr, *attn = nullptr, *act = nullptr, *part = nullptr;
+        unsigned* attn_count = nullptr;
+        sli::DevState* st = nullptr;  // [kPfLanes]: lane b feeds token st[b].token at position st[b].pos
+        float* ws = nullptr;
+        unsigned* cnt = nullptr;
+        sli::BgPlan qkv, wo, gu, down;
+        hipGraph_t graph = nullptr;
+        hipGraphExec_t exec = nullptr;
+    } pf;
     // SLI_EXEC_PERSISTENT (persist.h): the whole step as one launch
     int exec = SLI_EXEC_LAUNCHES;
     sli::PsArgs* ps_args = nullptr;  // device copy of the args record
@@ -99,6 +111,7 @@ struct sli_model {
 // device-side reduction over the ranks' buffers in rank order (the ranks' kernels are the multi-GPU
 // ones, so the sharded engine itself is what the group tests run).
 constexpr int kMaxGroup = 8;
+constexpr int kPfLanes = 8;  // prompt positions per prefill step (the MFMA projection's batch limit)
 struct sli_tp_group {
     int n = 0;
     int device = 0;
@@ -712,6 +725,61 @@ struct StepRecorder {
         SLI_HIP(hipGetLastError());
         return SLI_OK;
     }
+    // ---- prompt prefill (model.cpp:157-165 runs the prompt one token per forward): one step runs the
+    // layers for kPfLanes prompt positions of the one sequence at once — the projections as an MFMA
+    // skinny GEMM over the lanes (weights read once per kPfLanes positions), attention per lane over the
+    // shared cache up to the lane's own position (lane b sees the rows lanes < b wrote in the same qkv
+    // launch), K/V rows written where the decode step writes them. No LM head: the prompt's logits are
+    // not used (teacher forcing); the last prompt position runs as an ordinary decode step.
+    static BgIn bin_pf(sli_model* m, const float* x, const float* norm, int K) {
+        BgIn in{};
+        in.x = x;
+        in.norm_w = norm;
+        in.eps = m->c.eps;
+        in.K = K;
+        in.B = kPfLanes;
+        in.ws = m->pf.ws;
+        in.counters = m->pf.cnt;
+        return in;
+    }
+    static int prepare_prefill(sli_model* m) {
+        SLI_TRY((allow<BgEpiQKV<KT>, true>(m)));
+        SLI_TRY((allow<BgEpiStore, false>(m)));
+        SLI_TRY((allow<BgEpiSwiGLU, true>(m)));
+        return SLI_OK;
+    }
+    static int record_prefill(sli_model* m) {
+        if constexpr (!std::is_same<WT, __half>::value) {
+            return fail(SLI_ERR_ARG, "prefill needs fp16 weights");
+        } else {
+            auto& p = m->pf;
+            hipStream_t s = m->stream;
+            const int eb = std::min(64, (m->D + 255) / 256);
+            hipLaunchKernelGGL(embedding_batch_kernel<WT>, dim3(eb, kPfLanes), dim3(256), 0, s, p.st, (const WT*)m->emb,
+                               m->emb_s, p.x, m->V, m->D);
+            SLI_HIP(hipGetLastError());
+            const long long ls = (long long)m->hkv * m->T * m->hd;
+            for (int l = 0; l < m->L; ++l) {
+                const LayerW& w = m->layers[l];
+                KT* kc = (KT*)m->kc + (size_t)l * ls;
+                KT* vc = (KT*)m->vc + (size_t)l * ls;
+                BgEpiQKV<KT> eq{p.q, kc, vc, &p.st->pos, kPosStride, m->sin_t, m->cos_t, m->hq, m->hkv, m->hd, m->T};
+                eq.kv_seq = 0;  // every lane writes this sequence's cache
+                SLI_TRY(bg(m, w.qkv, bin_pf(m, p.x, m->norms + (size_t)(2 * l) * m->D, m->D), eq, p.qkv));
+                // lane b's kv heads [b*hkv, (b+1)*hkv) read cache heads [0, hkv) up to lane b's position
+                SLI_TRY(mha_launch<KT>(p.q, (const KT*)m->kc, (const KT*)m->vc, p.attn, l, 0, &p.st->pos, m->T, m->hd,
+                                       kPfLanes * m->hq, kPfLanes * m->hkv, m->hd, (long long)m->T * m->hd, ls, p.part,
+                                       p.attn_count, s, m->hkv, kPosStride, m->hkv));
+                BgEpiStore eo{p.x, p.x, nullptr, 1.0f, m->D, m->D};
+                SLI_TRY(bg(m, w.wo, bin_pf(m, p.attn, nullptr, m->hq * m->hd), eo, p.wo));
+                BgEpiSwiGLU eg{p.act, m->Il, m->c.act_mode};
+                SLI_TRY(bg(m, w.gu, bin_pf(m, p.x, m->norms + (size_t)(2 * l + 1) * m->D, m->D), eg, p.gu));
+                BgEpiStore ed{p.x, p.x, nullptr, 1.0f, m->D, m->D};
+                SLI_TRY(bg(m, w.down, bin_pf(m, p.act, nullptr, m->Il), ed, p.down));
+            }
+            return SLI_OK;
+        }
+    }
     // All weight-streaming launches of one step (for the roofline probe).
     static int gemvs(sli_model* m) {
         if (m->B > 1) {
@@ -828,6 +896,8 @@ static void destroy(sli_model* m) {
     if (m->stream) (void)hipStreamSynchronize(m->stream);
     if (m->graph_exec) (void)hipGraphExecDestroy(m->graph_exec);
     if (m->graph) (void)hipGraphDestroy(m->graph);
+    if (m->pf.exec) (void)hipGraphExecDestroy(m->pf.exec);
+    if (m->pf.graph) (void)hipGraphDestroy(m->pf.graph);
     if (m->comm) ncclCommDestroy(m->comm);
     for (void* p : m->allocs) (void)hipFree(p);
     if (m->stream && m->own_stream) (void)hipStreamDestroy(m->stream);
@@ -1157,6 +1227,108 @@ static int get_state(sli_model* m, int seq, int32_t* pos, int32_t* token, int32_
     if (error) *error = h[seq].error;
     return SLI_OK;
 }
+
+}  // extern "C" (reopened below)
+
+// ---------------------------------------------------------------- prompt prefill
+// MFMA prefill needs fp16 weights, batch 1 and no tensor parallelism; otherwise the prompt runs through the
+// decode step itself (teacher forcing), which gives the same tokens.
+static bool pf_supported(const sli_model* m) {
+    return m->c.w_dtype == SLI_DT_F16 && m->B == 1 && !m->partial && !m->group && m->D % 32 == 0 &&
+           m->Il % 32 == 0 && (m->hq * m->hd) % 32 == 0 && m->D <= kBgMaxStageK;
+}
+
+static int pf_setup(sli_model* m) {
+    auto& p = m->pf;
+    if (p.exec) return SLI_OK;
+    const int B = kPfLanes, D = m->D, hd = m->hd, cus = device_cus();
+    p.qkv = bg_plan((m->hq + 2 * m->hkv) * hd / 16, D, B, true, cus);
+    p.wo = bg_plan((D + 15) / 16, m->hq * hd, B, false, cus);
+    p.gu = bg_plan(m->Il / 8, D, B, true, cus);
+    p.down = bg_plan((D + 15) / 16, m->Il, B, false, cus);
+    size_t part = 0;
+    int groups = 1;
+    for (const BgPlan* q : {&p.qkv, &p.wo, &p.gu, &p.down}) {
+        if (q->groups <= 0) return fail(SLI_ERR_SHAPE, "prefill: no tiling fits");
+        part = std::max(part, bg_part_bytes(*q));
+        groups = std::max(groups, q->groups);
+    }
+    int rc = SLI_OK;
+    auto A = [&](void** ptr, size_t bytes) {
+        if (rc == SLI_OK) rc = model_alloc(m, ptr, bytes);
+    };
+    A((void**)&p.x, sizeof(float) * B * D);
+    A((void**)&p.q, sizeof(float) * B * m->hq * hd);
+    A((void**)&p.attn, sizeof(float) * B * m->hq * hd);
+    A((void**)&p.act, sizeof(float) * B * m->Il);
+    A((void**)&p.part, mha_part_bytes(m->T, B * m->hq, hd));
+    A((void**)&p.attn_count, sizeof(unsigned) * B * m->hkv);
+    A((void**)&p.st, sizeof(DevState) * B);
+    A((void**)&p.ws, part + 256);
+    A((void**)&p.cnt, sizeof(unsigned) * groups);
+    if (rc != SLI_OK) return rc;
+    SLI_HIP(hipMemset(p.attn_count, 0, sizeof(unsigned) * B * m->hkv));
+    SLI_HIP(hipMemset(p.cnt, 0, sizeof(unsigned) * groups));
+    SLI_TRY(SLI_DISPATCH(m, prepare_prefill, m));
+    return capture_graph(m->stream, p.graph, p.exec, [&]() { return SLI_DISPATCH(m, record_prefill, m); });
+}
+
+extern "C" int sli_model_prefill(sli_model* m, const int32_t* ids, int32_t n) {
+    SLI_CHECK(m && ids, SLI_ERR_ARG, "null argument");
+    SLI_CHECK(m->B == 1, SLI_ERR_STATE, "prefill: batch-1 models (a batch prefills through predict_batch)");
+    SLI_CHECK(n >= 1 && n <= m->T, SLI_ERR_RANGE, "prompt length out of range");
+    for (int i = 0; i < n; ++i)
+        SLI_CHECK(ids[i] >= 0 && ids[i] < m->V, SLI_ERR_RANGE, "Token index is greater than vocab size.");
+    SLI_HIP(hipSetDevice(m->c.device));
+    SLI_TRY(set_prompt(m, 0, ids, n));
+    SLI_HIP(hipMemcpyAsync(m->hist, ids, sizeof(int32_t) * n, hipMemcpyHostToDevice, m->stream));
+    if (n > 1 && pf_supported(m)) {
+        SLI_TRY(pf_setup(m));
+        // every chunk's lane states up front (positions 0 .. n-2; padding lanes repeat the last one): each
+        // chunk's copy reads host memory of its own, so the chunks are enqueued back to back, stream-ordered
+        const int steps = (n - 1 + kPfLanes - 1) / kPfLanes;
+        std::vector<DevState> lanes((size_t)steps * kPfLanes);
+        for (int c = 0; c < steps; ++c)
+            for (int b = 0; b < kPfLanes; ++b) {
+                const int p = std::min(c * kPfLanes + b, n - 2);
+                DevState& d = lanes[(size_t)c * kPfLanes + b];
+                d.pos = p;
+                d.token = ids[p];
+            }
+        for (int c = 0; c < steps; ++c) {
+            SLI_HIP(hipMemcpyAsync(m->pf.st, lanes.data() + (size_t)c * kPfLanes, sizeof(DevState) * kPfLanes,
+                                   hipMemcpyHostToDevice, m->stream));
+            SLI_HIP(hipGraphLaunch(m->pf.exec, m->stream));
+        }
+        SLI_HIP(hipStreamSynchronize(m->stream));
+    } else {
+        for (int p = 0; p < n - 1; ++p) {  // the decode step, teacher-forced (model.cpp:159-165)
+            SLI_TRY(set_state(m, 0, ids[p], p, 0));
+            SLI_TRY(sli_model_step(m));
+        }
+    }
+    // the last prompt position is an ordinary decode step: it yields the first greedy token
+    return set_state(m, 0, ids[n - 1], n - 1, 1);
+}
+
+extern "C" int sli_model_predict_prefill(sli_model* m, const int32_t* prompt, int32_t n_prompt, int32_t max_length,
+                                         int32_t* tokens_out, float* logits_out) {
+    SLI_CHECK(m && prompt && tokens_out, SLI_ERR_ARG, "null argument");
+    SLI_CHECK(max_length >= n_prompt && max_length <= m->T, SLI_ERR_RANGE, "max_length must be in [n_prompt, max_len]");
+    SLI_TRY(sli_model_prefill(m, prompt, n_prompt));
+    const size_t per_step = (size_t)m->v_n;
+    if (logits_out)  // positions the prefill computes no logits for
+        for (size_t i = 0; i < (size_t)(n_prompt - 1) * per_step; ++i) logits_out[i] = NAN;
+    for (int t = n_prompt - 1; t < max_length; ++t) {
+        SLI_TRY(sli_model_step(m));
+        if (logits_out) SLI_TRY(sli_model_get_logits(m, logits_out + (size_t)t * per_step, (int32_t)per_step, nullptr));
+    }
+    SLI_HIP(hipMemcpyAsync(tokens_out, m->hist, sizeof(int32_t) * max_length, hipMemcpyDeviceToHost, m->stream));
+    SLI_HIP(hipStreamSynchronize(m->stream));
+    return SLI_OK;
+}
+
+extern "C" {
 
 int sli_model_set_state(sli_model* m, int32_t token, int32_t pos, int32_t advance) {
     return set_state(m, -1, token, pos, advance);

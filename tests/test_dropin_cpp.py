@@ -63,3 +63,62 @@ def test_dropin_op_path_and_model_match_oracle(gpu, oracle, tmp_path, name):
         toks, logits = _read(out + suffix)
         assert np.array_equal(toks, otoks), suffix
         assert np.abs(logits - ologits).max() <= 1e-4, suffix
+
+
+L2_SRC = os.path.join(ROOT, "tests", "cpp", "level2_ops.cpp")
+L2_BIN = os.path.join(ROOT, "tests", "cpp", "_build", "level2_ops")
+
+
+def _compile_level2():
+    """INTEGRATION Level 2: an op-level client including the kernel headers by the reference's names."""
+    from simplellminference_amd import build
+    build.build()
+    if os.path.exists(L2_BIN) and os.path.getmtime(L2_BIN) >= max(os.path.getmtime(L2_SRC), os.path.getmtime(build.LIB)):
+        return L2_BIN
+    os.makedirs(os.path.dirname(L2_BIN), exist_ok=True)
+    inc = [f"-I{os.path.join(ROOT, 'include', d)}" for d in ("", "base", "memory", "op", "model", "kernel",
+                                                            "kernel/cpu", "kernel/cuda")]
+    cmd = ["hipcc", "--offload-arch=gfx950", "-O2", "-std=c++17", *inc, L2_SRC, "-o", L2_BIN,
+           f"-L{os.path.join(ROOT, 'simplellminference_amd')}", "-lsli",
+           "-Wl,-rpath,$ORIGIN/../../../simplellminference_amd"]
+    subprocess.run(cmd, check=True, capture_output=True, text=True)
+    return L2_BIN
+
+
+def test_level2_client_compiles_against_reference_header_names():
+    assert os.path.exists(_compile_level2())
+
+
+def _records(path):
+    raw = open(path, "rb").read()
+    out, i = {}, 0
+    while i < len(raw):
+        n = int(np.frombuffer(raw[i:i + 4], np.int32)[0])
+        name = raw[i + 4:i + 4 + n].decode()
+        i += 4 + n
+        m = int(np.frombuffer(raw[i:i + 4], np.int32)[0])
+        out[name] = np.frombuffer(raw[i + 4:i + 4 + 4 * m], np.float32).copy()
+        i += 4 + 4 * m
+    return out
+
+
+@pytest.mark.gpu
+def test_level2_launchers_match_oracle(gpu, oracle, tmp_path):
+    """Each kernel::*_kernel_cuda launcher (reference signatures, Tensor operands) against the oracle."""
+    path = str(tmp_path / "l2.bin")
+    r = subprocess.run([_compile_level2(), path], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    f = _records(path)
+    np.testing.assert_allclose(f["mm_y"], oracle.matmul(f["mm_x"], f["mm_w"].reshape(64, 256)), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(f["rms_y"], oracle.rmsnorm(f["rms_x"], f["rms_w"], 1e-5), rtol=2e-6, atol=1e-6)
+    ws, wc = oracle.rope_cache(64, 16, 10000.0)
+    assert np.array_equal(f["rope_sin"].view(np.uint32), ws.ravel().view(np.uint32))
+    assert np.array_equal(f["rope_cos"].view(np.uint32), wc.ravel().view(np.uint32))
+    wq, wk = oracle.rope(f["rope_q"], f["rope_k"], 5, ws, wc, 64)
+    np.testing.assert_allclose(f["rope_q_out"], wq, rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(f["rope_k_out"], wk, rtol=1e-6, atol=1e-6)
+    want = oracle.mha(f["mha_q"], f["mha_k"].reshape(2, 16, 128), f["mha_v"].reshape(2, 16, 128), 1, 9, 16, 64, 4, 2)
+    np.testing.assert_allclose(f["mha_out"], want, rtol=1e-5, atol=2e-6)
+    np.testing.assert_allclose(f["sw_out"], oracle.swiglu(f["sw_up"], f["sw_gate"]), rtol=2e-6, atol=1e-7)
+    assert np.array_equal(f["add_out"], oracle.add(f["add_a"], f["add_b"]))
+    assert np.array_equal(f["emb_out"], oracle.embedding(17, f["emb_table"].reshape(512, 256)))
