@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--exec", default="launches", choices=["launches", "persistent"],
                     help="launches: one graph of fused launches (default, fastest measured); persistent: the whole "
                          "step as one launch (batch 1, TP 1; DESIGN.md §4)")
+    ap.add_argument("--tp-allreduce", default="auto", choices=["auto", "rccl", "oneshot"],
+                    help="TP all-reduce: auto = the one-shot xGMI kernel if a validation step against RCCL agrees on "
+                         "every rank, else RCCL")
     ap.add_argument("--prefill-tokens", type=int, default=512,
                     help="after the decode timing: prefill a prompt of this many tokens (0: skip; batch 1 only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -127,6 +130,7 @@ def main():
     if dist_on:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
+    local = local % max(1, torch.cuda.device_count())  # (several ranks per GPU only in debug runs)
     torch.cuda.set_device(local)
 
     from simplellminference_amd.model import LlamaModel, comm_id, preset
@@ -152,6 +156,34 @@ def main():
         if dist_on:
             dist.barrier()
 
+    allreduce = "none"
+    if dist_on:
+        allreduce = "rccl"
+        if os.environ.get("SLI_DEBUG_NOCOMM") and a.tp_allreduce != "rccl":
+            # debug (several ranks on one GPU, no RCCL communicator): the one-shot kernels are the only exchange
+            from simplellminference_amd import tp
+            tp.open_oneshot(model)
+            model.set_allreduce("oneshot")
+            allreduce = "oneshot (SLI_DEBUG_NOCOMM: not validated against rccl)"
+        elif a.tp_allreduce != "rccl":
+            from simplellminference_amd import tp
+            import numpy as np
+            tp.open_oneshot(model)
+            model.step()  # RCCL reference step (idempotent: position ctx-1 is recomputed)
+            ref = model.logits()[0].copy()
+            model.set_allreduce("oneshot")
+            model.step()
+            got = model.logits()[0]
+            ok = bool(model.state()["error"] == 0 and np.isfinite(got).all() and np.abs(got - ref).max() <= 1e-3)
+            flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            if flag.item() == 1:
+                allreduce = "oneshot (validated against rccl on every rank)"
+            elif a.tp_allreduce == "oneshot":
+                raise SystemExit("one-shot all-reduce disagrees with RCCL")
+            else:
+                model.set_allreduce("rccl")
+                allreduce = "rccl (one-shot validation failed)"
     for _ in range(a.warmup):
         model.step()
     barrier()
@@ -232,6 +264,7 @@ def main():
                    "hbm_roofline_tokens_per_s": round(B * HBM_PEAK_GBS * 1e9 / (wbytes + kvbytes), 1),
                    "step_frac_of_hbm_peak": round((wbytes + kvbytes) / (ms * 1e-3) / (HBM_PEAK_GBS * 1e9), 4)},
         "exec": exec_mode,
+        "tp_allreduce": allreduce,
         "roofline": {"bound": "hbm", "kernel": f"{dom}: {FAMILY_KERNELS[B > 1][dom]}",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

@@ -144,6 +144,17 @@ typedef struct {
 int sli_tp_plan(const sli_model_config* cfg, int32_t kind, sli_shard_window* out);
 int sli_tp_vocab(const sli_model_config* cfg, int32_t* vocab_lo, int32_t* vocab_n);
 
+/* One-shot all-reduce over xGMI (replaces the step's RCCL all-reduces; one process per GPU): every rank
+ * exports its comm buffer (uncached device memory) with sli_model_comm_handle, the ranks exchange the
+ * handles over any host transport, each opens all of them with sli_model_comm_open (handles [nranks][
+ * sli_model_comm_handle_bytes()] in rank order) and switches with sli_model_set_allreduce. Each call
+ * pushes the rank's partial to every rank, raises a flag per rank, waits (bounded) for all flags and
+ * sums in rank order, so every rank holds bit-identical x; the argmax keys use the same exchange. */
+enum { SLI_ALLREDUCE_RCCL = 0, SLI_ALLREDUCE_ONESHOT = 1 };
+int sli_model_comm_handle_bytes(void);
+int sli_model_comm_handle(sli_model* m, void* out, int32_t n);
+int sli_model_comm_open(sli_model* m, const void* handles, int32_t nranks);
+int sli_model_set_allreduce(sli_model* m, int32_t mode);
 /* RCCL unique id for tensor parallelism (broadcast it from rank 0 with any host transport). */
 int sli_comm_id_bytes(void);
 int sli_comm_get_id(void* out);

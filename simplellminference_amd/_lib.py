@@ -104,6 +104,10 @@ _SIGS = {
     "sli_model_step_bytes": (c_int, [c_vp, P_d, P_d]),
     "sli_model_time_gemv": (c_int, [c_vp, c_i32, P_d, P_d, P_i32]),
     "sli_model_ps_stamps": (c_int, [c_vp, c_vp, c_i64, P_i32]),
+    "sli_model_comm_handle_bytes": (c_int, []),
+    "sli_model_comm_handle": (c_int, [c_vp, c_vp, c_i32]),
+    "sli_model_comm_open": (c_int, [c_vp, c_vp, c_i32]),
+    "sli_model_set_allreduce": (c_int, [c_vp, c_i32]),
     "sli_model_time_steps": (c_int, [c_vp, c_i32, P_d]),
     "sli_model_time_families": (c_int, [c_vp, c_i32, P_d, P_d, P_i32]),
     "sli_tp_group_create": (c_int, [ctypes.POINTER(ModelConfig), c_i32, ctypes.POINTER(c_vp)]),
@@ -146,6 +150,7 @@ def check(rc: int, where: str) -> None:
 def call(name: str, *args) -> int:
     rc = getattr(load(), name)(*args)
     if isinstance(rc, int) and name not in ("sli_version", "sli_mha_workspace_bytes", "sli_comm_id_bytes",
+                                                 "sli_model_comm_handle_bytes",
                                                  "sli_matmul_batch_workspace_bytes"):
         check(rc, name)
     return rc

@@ -28,6 +28,7 @@
 #include "bgemm.h"
 #include "common.h"
 #include "gemv.h"
+#include "oneshot.h"
 #include "ops_internal.h"
 #include "persist.h"
 #include "rope_table.h"
@@ -97,6 +98,14 @@ struct sli_model {
         hipGraph_t graph = nullptr;
         hipGraphExec_t exec = nullptr;
     } pf;
+    // tensor-parallel all-reduce: SLI_ALLREDUCE_RCCL (ncclAllReduce) or SLI_ALLREDUCE_ONESHOT (oneshot.h)
+    int ar_mode = SLI_ALLREDUCE_RCCL;
+    char* os_buf = nullptr;                  // this rank's comm buffer (uncached device memory, IPC-exported)
+    char* os_peer[sli::kOsMaxRanks] = {};    // every rank's buffer mapped here (own included)
+    bool os_open = false;
+    unsigned* os_epoch = nullptr;            // one-shot call counter
+    int os_nmax = 0;
+    size_t os_bytes = 0;
     // SLI_EXEC_PERSISTENT (persist.h): the whole step as one launch
     int exec = SLI_EXEC_LAUNCHES;
     sli::PsArgs* ps_args = nullptr;  // device copy of the args record
@@ -538,8 +547,27 @@ struct StepRecorder {
         SLI_HIP((launch_gemv_u<WT, 2, 4, NT>(w, in, e, (m->v_n + 1) / 2, m->stream)));
         return SLI_OK;
     }
+    static int oneshot(sli_model* m, const void* src, void* dst, int n, bool max_u64) {
+        OneShotArgs a{};
+        for (int r = 0; r < m->c.tp_size; ++r) a.peers[r] = m->os_peer[r];
+        a.rank = m->c.tp_rank;
+        a.nranks = m->c.tp_size;
+        a.n = n;
+        a.nmax = m->os_nmax;
+        a.src = (const float*)src;
+        a.dst = (float*)dst;
+        a.epoch = m->os_epoch;
+        a.st = m->st;
+        if (max_u64)
+            hipLaunchKernelGGL(oneshot_kernel<1>, dim3(1), dim3(1024), 0, m->stream, a);
+        else
+            hipLaunchKernelGGL(oneshot_kernel<0>, dim3(1), dim3(1024), 0, m->stream, a);
+        SLI_HIP(hipGetLastError());
+        return SLI_OK;
+    }
     static int allreduce_x(sli_model* m) {
         const size_t n = (size_t)m->B * m->D;
+        if (m->ar_mode == SLI_ALLREDUCE_ONESHOT) return oneshot(m, m->xpart, m->x, (int)n, false);
         if (m->collectives)
             SLI_NCCL(ncclAllReduce(m->xpart, m->x, n, ncclFloat32, ncclSum, m->comm, m->stream));
         else if (m->partial)  // debug no-comm mode: keep the local partial as the residual stream
@@ -682,6 +710,12 @@ struct StepRecorder {
         for (int p = 0; p < 2 * m->L; ++p) {
             SLI_TRY(record_phase(m, p));
             SLI_TRY(allreduce_x(m));
+        }
+        if (m->ar_mode == SLI_ALLREDUCE_ONESHOT) {  // the argmax keys through the same one-shot exchange
+            SLI_TRY(record_head(m, true));
+            void* k = m->B > 1 ? (void*)m->bkeys : (void*)&m->st->key;
+            SLI_TRY(oneshot(m, k, k, 2 * m->B, true));
+            return record_finalize(m);
         }
         if (!m->collectives) {
             SLI_TRY(record_head(m, m->B > 1));
@@ -899,6 +933,9 @@ static void destroy(sli_model* m) {
     if (m->pf.exec) (void)hipGraphExecDestroy(m->pf.exec);
     if (m->pf.graph) (void)hipGraphDestroy(m->pf.graph);
     if (m->comm) ncclCommDestroy(m->comm);
+    for (int r = 0; r < sli::kOsMaxRanks; ++r)
+        if (m->os_peer[r] && m->os_peer[r] != m->os_buf) (void)hipIpcCloseMemHandle(m->os_peer[r]);
+    if (m->os_buf) (void)hipFree(m->os_buf);
     for (void* p : m->allocs) (void)hipFree(p);
     if (m->stream && m->own_stream) (void)hipStreamDestroy(m->stream);
     delete m;
@@ -1563,6 +1600,67 @@ int sli_model_ps_stamps(sli_model* m, uint64_t* host, int64_t n, int32_t* grid) 
     SLI_TRY(ps_launch(a, (const PsArgs*)g.args, m->c.w_dtype, m->c.kv_dtype, m->ps_grid, m->ps_lds, m->stream, false));
     SLI_HIP(hipStreamSynchronize(m->stream));
     SLI_HIP(hipMemcpy(host, g.st, sizeof(uint64_t) * n, hipMemcpyDeviceToHost));
+    return SLI_OK;
+}
+
+// ---------------------------------------------------------------- one-shot all-reduce (oneshot.h)
+int sli_model_comm_handle(sli_model* m, void* out, int32_t n) {
+    SLI_CHECK(m && out, SLI_ERR_ARG, "null argument");
+    SLI_CHECK(n >= (int32_t)sizeof(hipIpcMemHandle_t), SLI_ERR_ARG, "handle buffer too small");
+    SLI_CHECK(m->c.tp_size > 1 && m->c.tp_size <= kOsMaxRanks && !m->group, SLI_ERR_STATE,
+              "one-shot all-reduce: 2..8 ranks, one process per rank");
+    SLI_HIP(hipSetDevice(m->c.device));
+    if (!m->os_buf) {
+        m->os_nmax = (std::max(m->B * m->D, 2 * m->B) + 3) & ~3;
+        m->os_bytes = 256 + sizeof(float) * 2 * (size_t)kOsMaxRanks * m->os_nmax;
+        SLI_HIP(hipExtMallocWithFlags((void**)&m->os_buf, m->os_bytes, hipDeviceMallocUncached));
+        SLI_HIP(hipMemset(m->os_buf, 0, m->os_bytes));
+        SLI_TRY(model_alloc(m, (void**)&m->os_epoch, sizeof(unsigned)));
+        SLI_HIP(hipMemset(m->os_epoch, 0, sizeof(unsigned)));
+    }
+    hipIpcMemHandle_t h;
+    SLI_HIP(hipIpcGetMemHandle(&h, m->os_buf));
+    std::memcpy(out, &h, sizeof(h));
+    return SLI_OK;
+}
+
+int sli_model_comm_handle_bytes(void) { return (int)sizeof(hipIpcMemHandle_t); }
+
+int sli_model_comm_open(sli_model* m, const void* handles, int32_t nranks) {
+    SLI_CHECK(m && handles, SLI_ERR_ARG, "null argument");
+    SLI_CHECK(m->os_buf, SLI_ERR_STATE, "call sli_model_comm_handle first");
+    SLI_CHECK(nranks == m->c.tp_size, SLI_ERR_ARG, "one handle per rank");
+    SLI_HIP(hipSetDevice(m->c.device));
+    if (m->os_open) return SLI_OK;
+    for (int r = 0; r < nranks; ++r) {
+        if (r == m->c.tp_rank) {
+            m->os_peer[r] = m->os_buf;
+            continue;
+        }
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, (const char*)handles + (size_t)r * sizeof(h), sizeof(h));
+        void* p = nullptr;
+        SLI_HIP(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+        m->os_peer[r] = (char*)p;
+    }
+    m->os_open = true;
+    return SLI_OK;
+}
+
+int sli_model_set_allreduce(sli_model* m, int32_t mode) {
+    SLI_CHECK(m, SLI_ERR_ARG, "null model");
+    SLI_CHECK(mode == SLI_ALLREDUCE_RCCL || mode == SLI_ALLREDUCE_ONESHOT, SLI_ERR_ARG, "unknown all-reduce mode");
+    SLI_CHECK(mode == SLI_ALLREDUCE_RCCL || m->os_open, SLI_ERR_STATE, "one-shot all-reduce: open the peers first");
+    SLI_CHECK(mode == SLI_ALLREDUCE_RCCL || m->exec == SLI_EXEC_LAUNCHES, SLI_ERR_STATE,
+              "tensor parallelism runs the launch graph");
+    if (mode != m->ar_mode) {
+        SLI_HIP(hipStreamSynchronize(m->stream));
+        if (m->graph_exec) (void)hipGraphExecDestroy(m->graph_exec);
+        if (m->graph) (void)hipGraphDestroy(m->graph);
+        m->graph_exec = nullptr;
+        m->graph = nullptr;
+        m->ar_mode = mode;
+    }
     return SLI_OK;
 }
 

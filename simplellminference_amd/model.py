@@ -171,6 +171,25 @@ class LlamaModel:
         call("sli_model_get_exec", self._h, ctypes.byref(v))
         return {i: k for k, i in self.EXEC.items()}[v.value]
 
+    # ------------------------------------------------------------------ tensor-parallel all-reduce
+    def comm_handle(self) -> bytes:
+        """This rank's one-shot all-reduce buffer as an IPC handle (exchange it with the other ranks)."""
+        n = _lib.load().sli_model_comm_handle_bytes()
+        buf = ctypes.create_string_buffer(n)
+        call("sli_model_comm_handle", self._h, buf, n)
+        return buf.raw
+
+    def comm_open(self, handles: list[bytes]) -> "LlamaModel":
+        blob = b"".join(handles)
+        buf = ctypes.create_string_buffer(blob, len(blob))
+        call("sli_model_comm_open", self._h, buf, len(handles))
+        return self
+
+    def set_allreduce(self, mode: str) -> "LlamaModel":
+        """"rccl" (ncclAllReduce in the step graph) or "oneshot" (oneshot.h, after comm_open)."""
+        call("sli_model_set_allreduce", self._h, {"rccl": 0, "oneshot": 1}[mode])
+        return self
+
     # ------------------------------------------------------------------ model.cpp:40-140
     def step(self):
         call("sli_model_step", self._h)

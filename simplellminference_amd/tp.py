@@ -45,3 +45,14 @@ def broadcast_comm_id(rank: int) -> bytes:
     box = [comm_id() if rank == 0 else None]
     dist.broadcast_object_list(box, src=0)
     return box[0]
+
+
+def open_oneshot(model) -> None:
+    """Exchange every rank's one-shot all-reduce buffer handle over the default process group (gloo) and
+    map the peers' buffers (sli_model_comm_open); the model then still all-reduces over RCCL until
+    set_allreduce("oneshot")."""
+    import torch.distributed as dist
+    mine = model.comm_handle()
+    allh = [None] * dist.get_world_size()
+    dist.all_gather_object(allh, mine)
+    model.comm_open(allh)

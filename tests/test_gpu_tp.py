@@ -128,3 +128,62 @@ def test_tp_rank_of_c2_shapes_steps_nocomm(gpu, monkeypatch, w, world):
     b = m.forward(1234, 2047)
     assert a.shape == (cfg.vocab_size // world,) and np.isfinite(a).all() and np.array_equal(a, b)
     m.close()
+
+
+def _oneshot_rank(rank, world, port, name, batch, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0",
+                      SLI_DEBUG_NOCOMM="1")  # no RCCL communicator: the one-shot kernels are the only exchange
+    import torch
+    import torch.distributed as dist
+
+    from simplellminference_amd import tp
+    from simplellminference_amd.model import LlamaModel, preset
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = rank % torch.cuda.device_count()
+        m = LlamaModel(config=preset(name), w_dtype="f16", kv_dtype="f16", tp_rank=rank, tp_size=world,
+                       device=dev, seed=0, batch=batch).init()
+        tp.open_oneshot(m)
+        m.set_allreduce("oneshot")
+        dist.barrier()
+        if batch == 1:
+            toks, logits = m.predict(PROMPT, 16, want_logits=True)
+        else:
+            toks, logits = m.predict_batch([PROMPT, [5, 6, 7]][:batch], 16, want_logits=True)
+        err = m.state()["error"]
+        parts = [torch.zeros(logits.shape, dtype=torch.float32) for _ in range(world)]
+        dist.all_gather(parts, torch.from_numpy(np.ascontiguousarray(logits)))
+        dist.barrier()
+        m.close()
+        if rank == 0:
+            q.put(("ok", toks, np.concatenate([p.numpy() for p in parts], axis=-1), err))
+    except Exception as e:  # report to the parent instead of hanging it
+        q.put(("err", repr(e), None, None))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name,batch", [("tiny", 1), ("tiny-gqa", 1), ("tiny-gqa", 2)])
+def test_oneshot_allreduce_two_processes(gpu, name, batch):
+    """The one-shot all-reduce (oneshot.h) between two rank PROCESSES through IPC-mapped uncached buffers
+    (both on device 0 here; on the 8-GPU node each on its own GPU, over xGMI): greedy tokens identical to
+    the TP = 1 engine, logits within 1e-3, no device error (the bounded waits never gave up)."""
+    from simplellminference_amd.model import LlamaModel, preset
+    ref = LlamaModel(config=preset(name), w_dtype="f16", kv_dtype="f16", seed=0, batch=batch).init()
+    if batch == 1:
+        rtoks, rlogits = ref.predict(PROMPT, 16, want_logits=True)
+    else:
+        rtoks, rlogits = ref.predict_batch([PROMPT, [5, 6, 7]][:batch], 16, want_logits=True)
+    ref.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_oneshot_rank, args=(r, 2, port, name, batch, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    status, toks, logits, err = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+    assert status == "ok", toks
+    assert err == 0
+    assert np.array_equal(toks, rtoks)
+    assert np.abs(logits - rlogits).max() <= 1e-3
