@@ -36,6 +36,8 @@ struct AttnArgs {
     unsigned long long* stamps = nullptr;  // diagnostic (tools/attn_lab): per-workgroup s_memrealtime x4
     int cache_heads = 0;    // > 0: the cache holds cache_heads kv heads shared by every sequence (prefill lanes
                             // of one sequence): kv head kvh reads cache head kvh % cache_heads
+    int defer_merge = 0;    // 1: only write the workgroup partials (plain stores); the consumer merges the
+                            // splits (the wo GEMV's input staging, gemv.h XStageMerge) after the launch
 };
 
 // Position of the sequence that owns (batched) kv head kvh.
@@ -178,6 +180,28 @@ __device__ __forceinline__ bool attn_publish(const AttnArgs<KT>& a, int kvh, int
         }
     }
     __syncthreads();
+    if (a.defer_merge) {  // partials for the next launch (the kernel boundary publishes them): plain stores
+        for (int i = threadIdx.x; i < G * HD; i += 64 * WAVES) {
+            const int g = i / HD, d = i - g * HD;
+            float M = -INFINITY;
+#pragma unroll
+            for (int w = 0; w < WAVES; ++w) M = fmaxf(M, sh[w][g][HD]);
+            float o = 0.0f, L = 0.0f;
+#pragma unroll
+            for (int w = 0; w < WAVES; ++w) {
+                const float c = expf(sh[w][g][HD] - M);
+                o = fmaf(c, sh[w][g][d], o);
+                L = fmaf(c, sh[w][g][HD + 1], L);
+            }
+            float* dst = a.part + ((size_t)(kvh * G + g) * a.max_splits + wgs) * (HD + kAttnPartPad);
+            dst[d] = o;
+            if (d == 0) {
+                dst[HD] = M;
+                dst[HD + 1] = L;
+            }
+        }
+        return false;
+    }
     // Workgroup partial: the WAVES slice states merged in LDS, published write-through (sc1) so the
     // head's last-arriving workgroup can read it from any XCD without a fence pair
     // (MI355X_MICROARCH.md, hand-off table row 1: sc1 stores, drained, one agent-scope add per

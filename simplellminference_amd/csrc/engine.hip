@@ -516,13 +516,21 @@ struct StepRecorder {
         SLI_HIP((launch_gemv_u<WT, 2, 4, NT>((const WT*)w.qkv, in, e, (m->hq + 2 * m->hkv) * (m->hd / 2), m->stream)));
         return SLI_OK;
     }
+    // wo + residual; its input is merged from the attention's split partials while it is staged
+    // (attention launched with defer_merge, gemv.h XStageMerge)
     static int gemv_wo(sli_model* m, int l) {
         const LayerW& w = m->layers[l];
         const bool tp = m->partial;
         GemvIn in{m->attn, nullptr, 0.0f, m->hq * m->hd};
         EpiStore<1> e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, w.wo_s, 1.0f, m->D};
-        SLI_HIP((launch_gemv_u<WT, 1, 2, NT>((const WT*)w.wo, in, e, m->D, m->stream)));
+        const AttnMergeIn am{m->part, &m->st->pos, attn_max_splits(m), attn_wg_positions(m->c.kv_dtype, m->hd), m->hd};
+        constexpr int UW = std::is_same<WT, int8_t>::value ? 1 : 2;
+        SLI_HIP((launch_gemv_merge<WT, 1, UW, NT>((const WT*)w.wo, in, e, am, m->D, m->stream)));
         return SLI_OK;
+    }
+    static int attn_max_splits(sli_model* m) {
+        const int ppwg = attn_wg_positions(m->c.kv_dtype, m->hd);
+        return (m->T + ppwg - 1) / ppwg;
     }
     static int gemv_gu(sli_model* m, int l) {
         const LayerW& w = m->layers[l];
@@ -662,7 +670,7 @@ struct StepRecorder {
             // a batch is B * hkv kv heads of one layer: sequence b owns kv heads [b*hkv, (b+1)*hkv)
             SLI_TRY(mha_launch<KT>(m->q, (const KT*)m->kc, (const KT*)m->vc, m->attn, l, 0, &m->st->pos, m->T, m->hd,
                                    m->B * m->hq, m->B * m->hkv, ps, hs, ls, m->part, m->attn_count, s,
-                                   batched ? m->hkv : 0, batched ? kPosStride : 0));
+                                   batched ? m->hkv : 0, batched ? kPosStride : 0, 0, batched ? 0 : 1));
             return batched ? b_wo(m, l) : gemv_wo(m, l);
         }
         SLI_TRY(batched ? b_gu(m, l) : gemv_gu(m, l));
@@ -846,7 +854,8 @@ struct StepRecorder {
                     const long long ls = (long long)m->B * m->hkv * m->T * m->hd;
                     SLI_TRY(mha_launch<KT>(m->q, (const KT*)m->kc, (const KT*)m->vc, m->attn, l, 0, &m->st->pos, m->T,
                                            m->hd, m->B * m->hq, m->B * m->hkv, ps, hs, ls, m->part, m->attn_count,
-                                           m->stream, batched ? m->hkv : 0, batched ? kPosStride : 0));
+                                           m->stream, batched ? m->hkv : 0, batched ? kPosStride : 0, 0,
+                                           batched ? 0 : 1));
                     break;
                 }
                 case SLI_FAM_WO: SLI_TRY(batched ? b_wo(m, l) : gemv_wo(m, l)); break;

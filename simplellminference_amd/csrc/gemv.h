@@ -107,6 +107,88 @@ struct XStage {
 };
 
 
+// The wo GEMV's input staged straight from the attention's split partials (attention.h, defer_merge): for
+// every head h and dim d, out = (sum_s e^{m_s - M} o_s) / (sum_s e^{m_s - M} l_s) over the ns live splits in
+// split order, M = max_s m_s — attn_merge's arithmetic, so the result is bit-identical to the attention
+// kernel's own last-arriver merge, without that merge's serial tail (an arrival counter, a second round
+// trip to the partials and a store) inside the attention launch. The partials are loaded with the input
+// loads, before the weight stream, like XStage's x (NS splits in flight per thread, the rest from memory).
+struct AttnMergeIn {
+    const float* part;       // [heads][max_splits][hd + kAttnPartPad]
+    const int32_t* pos_dev;  // the live context: ns = min(pos / ppwg + 1, max_splits)
+    int max_splits, ppwg, hd;
+};
+
+template <int G, int NS = 8>
+struct XStageMerge {
+    AttnMergeIn am;
+    float4 ov[NS];
+    float2 ml[NS];
+    int pos = 0;
+    __device__ __forceinline__ const float* row(int f, int s) const {
+        const int h = f / (am.hd >> 2);
+        return am.part + ((size_t)h * am.max_splits + min(s, am.max_splits - 1)) * (am.hd + kAttnPartPad);
+    }
+    __device__ __forceinline__ void issue(const GemvIn& in) {
+        const int f = min((int)threadIdx.x, (in.cols >> 2) - 1);  // the first round of the input
+        const int d4 = f % (am.hd >> 2);
+        pos = *am.pos_dev;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const float* r = row(f, s);
+            ov[s] = reinterpret_cast<const float4*>(r)[d4];
+            ml[s] = *reinterpret_cast<const float2*>(r + am.hd);
+        }
+    }
+    struct Acc {
+        float M;
+        float4 o = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        float L = 0.0f;
+        __device__ __forceinline__ void add(float2 lm, float4 v) {
+            const float w = expf(lm.x - M);
+            o.x = fmaf(w, v.x, o.x);
+            o.y = fmaf(w, v.y, o.y);
+            o.z = fmaf(w, v.z, o.z);
+            o.w = fmaf(w, v.w, o.w);
+            L = fmaf(w, lm.y, L);
+        }
+        __device__ __forceinline__ float4 out() const { return make_float4(o.x / L, o.y / L, o.z / L, o.w / L); }
+    };
+    // the first round: splits < NS from the registers (unrolled and predicated: no dynamic register index)
+    __device__ __forceinline__ float4 merge_regs(int f, int ns) const {
+        const int d4 = f % (am.hd >> 2);
+        float M = -INFINITY;
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+            if (s < ns) M = fmaxf(M, ml[s].x);
+        for (int s = NS; s < ns; ++s) M = fmaxf(M, row(f, s)[am.hd]);
+        Acc a{M};
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+            if (s < ns) a.add(ml[s], ov[s]);
+        for (int s = NS; s < ns; ++s)
+            a.add(*reinterpret_cast<const float2*>(row(f, s) + am.hd), reinterpret_cast<const float4*>(row(f, s))[d4]);
+        return a.out();
+    }
+    // later rounds (inputs wider than 4 * kGemvThreads): straight from memory
+    __device__ __forceinline__ float4 merge_mem(int f, int ns) const {
+        const int d4 = f % (am.hd >> 2);
+        float M = -INFINITY;
+        for (int s = 0; s < ns; ++s) M = fmaxf(M, row(f, s)[am.hd]);
+        Acc a{M};
+        for (int s = 0; s < ns; ++s)
+            a.add(*reinterpret_cast<const float2*>(row(f, s) + am.hd), reinterpret_cast<const float4*>(row(f, s))[d4]);
+        return a.out();
+    }
+    __device__ __forceinline__ void commit(float* smem, const GemvIn& in) {
+        float4* xs4 = reinterpret_cast<float4*>(smem + kGemvLdsHead);
+        const int n4 = in.cols >> 2;
+        const int ns = min(pos / am.ppwg + 1, am.max_splits);
+        if ((int)threadIdx.x < n4) xs4[xswz<G>(threadIdx.x)] = merge_regs(threadIdx.x, ns);
+        for (int f = threadIdx.x + kGemvThreads; f < n4; f += kGemvThreads) xs4[xswz<G>(f)] = merge_mem(f, ns);
+    }
+};
+
 // One-shot staging for callers that have nothing to overlap it with.
 template <int G = 1>
 __device__ __forceinline__ void gemv_stage_x(float* smem, const GemvIn& in) {
@@ -296,6 +378,16 @@ __global__ void __launch_bounds__(kGemvThreads) gemv_kernel(const WT* __restrict
     Epi epi = epi_in;  // mutable per-thread copy (EpiLogits keeps a running key)
     extern __shared__ __attribute__((aligned(16))) float smem[];
     XStage<Vec16<WT>::N / 4> stage;
+    gemv_block<WT, R, U, NT>(W, in, epi, stage, smem);
+}
+
+// the wo GEMV with its input merged from the attention's split partials (XStageMerge)
+template <typename WT, int R, int U, bool NT, class Epi>
+__global__ void __launch_bounds__(kGemvThreads) gemv_merge_kernel(const WT* __restrict__ W, GemvIn in, Epi epi_in,
+                                                                  AttnMergeIn am) {
+    Epi epi = epi_in;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    XStageMerge<Vec16<WT>::N / 4> stage{am};
     gemv_block<WT, R, U, NT>(W, in, epi, stage, smem);
 }
 
@@ -542,6 +634,15 @@ inline int gemv_blocks(int units) {
     const int maxb = gemv_max_blocks();
     int b = (units + (kGemvThreads / 64) - 1) / (kGemvThreads / 64);
     return b < maxb ? (b > 0 ? b : 1) : maxb;
+}
+
+template <typename WT, int R, int U, bool NT, class Epi>
+hipError_t launch_gemv_merge(const WT* W, const GemvIn& in, const Epi& epi, const AttnMergeIn& am, int units,
+                             hipStream_t s) {
+    const int grid = gemv_blocks(units);
+    const size_t lds = gemv_lds_bytes(in.cols) + sizeof(float) * gemv_res_floats(units, grid, R);
+    hipLaunchKernelGGL((gemv_merge_kernel<WT, R, U, NT, Epi>), dim3(grid), dim3(kGemvThreads), lds, s, W, in, epi, am);
+    return hipGetLastError();
 }
 
 template <typename WT, int R, int U, bool NT, class Epi>

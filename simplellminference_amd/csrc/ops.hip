@@ -164,7 +164,7 @@ template <typename KT, int HD>
 static int mha_launch_hd(const float* q, const KT* kc, const KT* vc, float* out, int layer, int pos, const int32_t* pos_dev,
                          int T, int H, int Hkv, long long pos_stride, long long head_stride, long long layer_stride,
                          float* part, unsigned* counters, hipStream_t s, int seq_heads, int pos_seq_stride,
-                         int cache_heads) {
+                         int cache_heads, int defer_merge) {
     using Geo = AttnGeom<KT, HD>;
     constexpr int ppw_wg = Geo::PPWG;
     const int wg_splits = (T + ppw_wg - 1) / ppw_wg;
@@ -173,6 +173,7 @@ static int mha_launch_hd(const float* q, const KT* kc, const KT* vc, float* out,
                    head_stride, part, out, counters, pos_dev, pos, Hkv, wg_splits, 1.0f / sqrtf((float)HD),
                    seq_heads > 0 ? seq_heads : Hkv, pos_seq_stride};
     a.cache_heads = cache_heads;
+    a.defer_merge = defer_merge;
     const int blocks = Hkv * wg_splits;
     const int g = H / Hkv;
     switch (g) {
@@ -189,22 +190,23 @@ static int mha_launch_hd(const float* q, const KT* kc, const KT* vc, float* out,
 template <typename KT>
 int mha_launch(const float* q, const KT* kc, const KT* vc, float* out, int layer, int pos, const int32_t* pos_dev,
                int T, int hd, int H, int Hkv, long long pos_stride, long long head_stride, long long layer_stride,
-               float* part, unsigned* counters, hipStream_t s, int seq_heads, int pos_seq_stride, int cache_heads) {
+               float* part, unsigned* counters, hipStream_t s, int seq_heads, int pos_seq_stride, int cache_heads,
+               int defer_merge) {
     if (hd == 128)
         return mha_launch_hd<KT, 128>(q, kc, vc, out, layer, pos, pos_dev, T, H, Hkv, pos_stride, head_stride,
-                                      layer_stride, part, counters, s, seq_heads, pos_seq_stride, cache_heads);
+                                      layer_stride, part, counters, s, seq_heads, pos_seq_stride, cache_heads, defer_merge);
     if (hd == 64)
         return mha_launch_hd<KT, 64>(q, kc, vc, out, layer, pos, pos_dev, T, H, Hkv, pos_stride, head_stride,
-                                     layer_stride, part, counters, s, seq_heads, pos_seq_stride, cache_heads);
+                                     layer_stride, part, counters, s, seq_heads, pos_seq_stride, cache_heads, defer_merge);
     return fail(SLI_ERR_SHAPE, "mha: head_dim must be 64 or 128");
 }
 
 template int mha_launch<float>(const float*, const float*, const float*, float*, int, int, const int32_t*, int, int,
                                int, int, long long, long long, long long, float*, unsigned*, hipStream_t, int, int,
-                               int);
+                               int, int);
 template int mha_launch<__half>(const float*, const __half*, const __half*, float*, int, int, const int32_t*, int,
                                 int, int, int, long long, long long, long long, float*, unsigned*, hipStream_t, int,
-                                int, int);
+                                int, int, int);
 
 size_t mha_part_bytes(int T, int H, int hd) {
     const int ppw_wg_min = attn_wg_positions(SLI_DT_F32, hd);
