@@ -69,10 +69,12 @@ def parse():
                          "every rank, else RCCL")
     ap.add_argument("--prefill-tokens", type=int, default=512,
                     help="after the decode timing: prefill a prompt of this many tokens (0: skip; batch 1 only)")
+    ap.add_argument("--prefill-reps", type=int, default=3, help="timed prefill repetitions (after one warm-up)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--greedy-steps", type=int, default=64, help="the greedy sanity run's length (profiling passes: 2)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample budget")
     ap.add_argument("--gemv-iters", type=int, default=20)
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r04_gemv_traffic.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r2_gemv_traffic.json"))
     return ap.parse_args()
 
 
@@ -217,7 +219,7 @@ def main():
 
     # a true greedy decode beside the idempotent-step timing: 64 tokens at positions ctx-64 .. ctx-1, the
     # state (position, next token = greedy argmax) advancing on the device every step
-    g_steps = min(64, a.ctx - 1)
+    g_steps = min(a.greedy_steps, a.ctx - 1)
     for b in range(B):
         model.set_state_seq(b, 1234 + 17 * b, a.ctx - 1 - g_steps, advance=True)
     barrier()
@@ -304,7 +306,7 @@ def main():
         model.prefill(ids)  # warm-up: capture + first run
         barrier()
         tp = time.perf_counter()
-        reps = 3
+        reps = a.prefill_reps
         for _ in range(reps):
             model.prefill(ids)
         barrier()

@@ -524,7 +524,7 @@ struct StepRecorder {
         GemvIn in{m->attn, nullptr, 0.0f, m->hq * m->hd};
         EpiStore<1> e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, w.wo_s, 1.0f, m->D};
         const AttnMergeIn am{m->part, &m->st->pos, attn_max_splits(m), attn_wg_positions(m->c.kv_dtype, m->hd), m->hd};
-        constexpr int UW = std::is_same<WT, int8_t>::value ? 1 : 2;
+        constexpr int UW = 2;  // int8 too (tools/gemv_lab i8: R1U2 7.5 us vs R1U1 7.95 on the 4096x4096 shape)
         SLI_HIP((launch_gemv_merge<WT, 1, UW, NT>((const WT*)w.wo, in, e, am, m->D, m->stream)));
         return SLI_OK;
     }
@@ -544,7 +544,10 @@ struct StepRecorder {
         const bool tp = m->partial;
         GemvIn in{m->act, nullptr, 0.0f, m->Il};
         EpiStore<1> e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, w.down_s, 1.0f, m->D};
-        SLI_HIP((launch_gemv_u<WT, 1, 6, NT>((const WT*)w.down, in, e, m->D, m->stream)));
+        if constexpr (std::is_same<WT, int8_t>::value)  // tools/gemv_lab i8: R1U4 11.66 us vs R1U3 11.74
+            SLI_HIP((launch_gemv<WT, 1, 4, NT>((const WT*)w.down, in, e, m->D, m->stream)));
+        else
+            SLI_HIP((launch_gemv_u<WT, 1, 6, NT>((const WT*)w.down, in, e, m->D, m->stream)));
         return SLI_OK;
     }
     static int lm_head_blocks(sli_model* m) { return gemv_blocks((m->v_n + 1) / 2); }

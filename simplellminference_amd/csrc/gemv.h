@@ -369,7 +369,9 @@ __device__ __forceinline__ void gemv_block(const WT* __restrict__ W, const GemvI
         p[0] = t_entry;
         p[1] = t_staged;
         p[2] = __builtin_amdgcn_s_memrealtime();
-        p[3] = (unsigned long long)max(nsteps, 1);
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        p[3] = (unsigned long long)max(nsteps, 1) | ((unsigned long long)(xcc & 15) << 32);  // diagnostic: XCD
     }
 }
 

@@ -194,6 +194,80 @@ int main(int argc, char** argv) {
                1000 * cold / NL, 1000 * str / NL, 1000 * both / NL, 1000 * (both - str) / NL, 1000 * (both2 - str) / NL);
         return 0;
     }
+    if (mode == "i8") {
+        // int8 weights (the fp16 buffers reinterpreted: half their bytes), every (R, U) on each shape, and the
+        // streaming-read ceiling of the same bytes
+        using I8Run = std::function<void(const int8_t*, const GemvIn&, float*, int, hipStream_t)>;
+        auto mk = [](auto r_tag, auto u_tag) -> I8Run {
+            constexpr int R = decltype(r_tag)::value, U = decltype(u_tag)::value;
+            return [](const int8_t* W, const GemvIn& in, float* y, int rows, hipStream_t s) {
+                EpiStore<R> e{y, nullptr, nullptr, 1.0f, rows};
+                CK((launch_gemv<int8_t, R, U, true>(W, in, e, (rows + R - 1) / R, s)));
+            };
+        };
+        using I1 = std::integral_constant<int, 1>;
+        using I2 = std::integral_constant<int, 2>;
+        using I3 = std::integral_constant<int, 3>;
+        using I4 = std::integral_constant<int, 4>;
+        std::vector<std::pair<const char*, I8Run>> cf = {
+            {"R1U1", mk(I1{}, I1{})}, {"R1U2", mk(I1{}, I2{})}, {"R1U3", mk(I1{}, I3{})}, {"R1U4", mk(I1{}, I4{})},
+            {"R2U1", mk(I2{}, I1{})}, {"R2U2", mk(I2{}, I2{})}, {"R2U3", mk(I2{}, I3{})}, {"R4U1", mk(I4{}, I1{})},
+            {"R4U2", mk(I4{}, I2{})}};
+        for (int si = 0; si < 4; ++si) {
+            const Shape& sh = kShapes[si];
+            const double bytes = (double)sh.rows * sh.cols;
+            for (auto& c : cf) {
+                const float ms = time_graph(s, [&] {
+                    for (int l = 0; l < NL; ++l) c.second((const int8_t*)w[si][l], in_for0(si), y, sh.rows, s);
+                });
+                const double us = 1000.0 * ms / NL;
+                printf("i8 %-5s %-6s %8.2f us  %7.1f GB/s\n", sh.name, c.first, us, bytes / (us * 1e-6) / 1e9);
+            }
+            const float ms = time_graph(s, [&] {
+                for (int l = 0; l < NL; ++l)
+                    hipLaunchKernelGGL(stream_kernel<8>, dim3(256), dim3(1024), 0, s, (const char*)w[si][l],
+                                       (long long)bytes, y2, nullptr);
+            });
+            const double us = 1000.0 * ms / NL;
+            printf("i8 %-5s %-6s %8.2f us  %7.1f GB/s\n", sh.name, "stream", us, bytes / (us * 1e-6) / 1e9);
+        }
+        return 0;
+    }
+    if (mode == "tail") {
+        // raw per-wave stamps (entry, staged, exit, steps | xcd << 32) of the R1U4 GEMV on every shape, launches
+        // 2..NL-1, written to argv[2] for offline analysis (tools/gemv_tail.py)
+        const int nst = 256 * 16 * 4;
+        unsigned long long* st;
+        CK(hipMalloc(&st, (size_t)NL * nst * 8));
+        std::vector<unsigned long long> h((size_t)NL * nst);
+        FILE* f = fopen(argc > 2 ? argv[2] : "gpurun_out/gemv_tail.bin", "wb");
+        for (int si : {0, 1, 2, 3}) {
+            const Shape& sh = kShapes[si];
+            for (int R : {1, 2}) {
+                CK(hipMemset(st, 0, (size_t)NL * nst * 8));
+                time_graph(s, [&] {
+                    for (int l = 0; l < NL; ++l) {
+                        GemvIn in = in_for0(si);
+                        in.stamps = st + (size_t)l * nst;
+                        if (R == 1) {
+                            EpiStore<1> e{y, nullptr, nullptr, 1.0f, sh.rows};
+                            CK((launch_gemv<__half, 1, 4, true>(w[si][l], in, e, sh.rows, s)));
+                        } else {
+                            EpiStore<2> e{y, nullptr, nullptr, 1.0f, sh.rows};
+                            CK((launch_gemv<__half, 2, 4, true>(w[si][l], in, e, sh.rows / 2, s)));
+                        }
+                    }
+                }, 1);
+                CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+                const int hdr[3] = {si, R, NL};
+                fwrite(hdr, 4, 3, f);
+                fwrite(h.data(), 8, h.size(), f);
+            }
+        }
+        fclose(f);
+        printf("wrote stamps\n");
+        return 0;
+    }
     if (mode == "probe") {
         unsigned long long* o;
         CK(hipMalloc(&o, 256 * 8));

@@ -18,7 +18,7 @@ for r in csv.DictReader(open(path)):
         continue
     per[r["Kernel_Name"]].append(float(r["Counter_Value"]))
 def weight_kernel(k):  # the step's weight-streaming kernels: batch-1 GEMV or the batched MFMA projection
-    return "gemv_kernel" in k or "bgemm_kernel" in k
+    return "gemv_kernel" in k or "gemv_merge_kernel" in k or "bgemm_kernel" in k
 
 
 gemv = [v for k, vs in per.items() if weight_kernel(k) for v in vs]
@@ -50,8 +50,10 @@ def family(k):
     for tag, fam in (("EpiQKV", "qkv"), ("EpiSwiGLU", "gate_up"), ("EpiLogits", "lm_head")):
         if tag in k and weight_kernel(k):
             return fam
-    if "gemv_kernel" in k and "EpiStore<1>" in k:  # wo streams U = 2 vectors per lane, down U = 6
-        return "wo" if ", 1, 2, true" in k else "down" if ", 1, 6, true" in k else None
+    if "gemv_merge_kernel" in k:  # wo: its input staged from the attention's split partials
+        return "wo"
+    if "gemv_kernel" in k and "EpiStore<1>" in k:  # the only other single-row residual GEMV of a step
+        return "down"
     if "bgemm_kernel" in k and "BgEpiStore" in k:
         return "wo+down"  # one instantiation serves both batched row-parallel projections
     return None
