@@ -36,8 +36,9 @@ struct AttnArgs {
     unsigned long long* stamps = nullptr;  // diagnostic (tools/attn_lab): per-workgroup s_memrealtime x4
     int cache_heads = 0;    // > 0: the cache holds cache_heads kv heads shared by every sequence (prefill lanes
                             // of one sequence): kv head kvh reads cache head kvh % cache_heads
-    int defer_merge = 0;    // 1: only write the workgroup partials (plain stores); the consumer merges the
-                            // splits (the wo GEMV's input staging, gemv.h XStageMerge) after the launch
+    int defer_merge = 0;    // != 0: only write the workgroup partials (plain stores); the splits are merged
+                            // after the launch: 1 by the consumer (the wo GEMV's input staging, gemv.h
+                            // XStageMerge), 2 by attn_merge_kernel (mha_launch launches it)
 };
 
 // Position of the sequence that owns (batched) kv head kvh.
@@ -314,6 +315,18 @@ __global__ void __launch_bounds__(64 * WAVES) attn_partial_kernel(AttnArgs<KT> a
         attn_merge<HD, G>(a.part, a.out, kvh, a.max_splits, attn_live_splits<KT, HD, G>(a, kvh), 0, 64 * WAVES);
         if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 4 + 3] = __builtin_amdgcn_s_memrealtime();
     }
+}
+
+// The split merge as its own launch after an attention launch with defer_merge (batched decode: the
+// consumer is the MFMA projection, whose every workgroup stages the whole activation, so merging in its
+// staging would re-read the partials once per workgroup). Freed of the merge, the attention workgroups
+// end right after their partial store: at C4 the 1024 workgroups run in two residency rounds, and the
+// first round's slots free sooner. grid: n_kv_heads workgroups of kAttnMergeThreads.
+constexpr int kAttnMergeThreads = 256;
+template <typename KT, int HD, int G>
+__global__ void __launch_bounds__(kAttnMergeThreads) attn_merge_kernel(AttnArgs<KT> a) {
+    const int kvh = blockIdx.x;
+    attn_merge<HD, G>(a.part, a.out, kvh, a.max_splits, attn_live_splits<KT, HD, G>(a, kvh), 0, kAttnMergeThreads);
 }
 
 }  // namespace sli

@@ -504,6 +504,16 @@ static hipError_t launch_gemv_u(const WT* W, const GemvIn& in, const Epi& epi, i
     return launch_gemv<WT, R, UW, NT>(W, in, epi, units, s);
 }
 
+// batched decode: the attention's split merge as its own launch (attention.h attn_merge_kernel, mode 2);
+// SLI_ATTN_MERGE_LAUNCH=0 keeps the last-arriver merge inside the attention launch (A/B measurement)
+static int defer_batched() {
+    static const int v = [] {
+        const char* e = getenv("SLI_ATTN_MERGE_LAUNCH");
+        return e && e[0] == '0' ? 0 : 2;
+    }();
+    return v;
+}
+
 template <typename WT, typename KT>
 struct StepRecorder {
     static constexpr bool NT = true;  // streamed-once weights: non-temporal loads
@@ -673,7 +683,7 @@ struct StepRecorder {
             // a batch is B * hkv kv heads of one layer: sequence b owns kv heads [b*hkv, (b+1)*hkv)
             SLI_TRY(mha_launch<KT>(m->q, (const KT*)m->kc, (const KT*)m->vc, m->attn, l, 0, &m->st->pos, m->T, m->hd,
                                    m->B * m->hq, m->B * m->hkv, ps, hs, ls, m->part, m->attn_count, s,
-                                   batched ? m->hkv : 0, batched ? kPosStride : 0, 0, batched ? 0 : 1));
+                                   batched ? m->hkv : 0, batched ? kPosStride : 0, 0, batched ? defer_batched() : 1));
             return batched ? b_wo(m, l) : gemv_wo(m, l);
         }
         SLI_TRY(batched ? b_gu(m, l) : gemv_gu(m, l));
@@ -858,7 +868,7 @@ struct StepRecorder {
                     SLI_TRY(mha_launch<KT>(m->q, (const KT*)m->kc, (const KT*)m->vc, m->attn, l, 0, &m->st->pos, m->T,
                                            m->hd, m->B * m->hq, m->B * m->hkv, ps, hs, ls, m->part, m->attn_count,
                                            m->stream, batched ? m->hkv : 0, batched ? kPosStride : 0, 0,
-                                           batched ? 0 : 1));
+                                           batched ? defer_batched() : 1));
                     break;
                 }
                 case SLI_FAM_WO: SLI_TRY(batched ? b_wo(m, l) : gemv_wo(m, l)); break;
