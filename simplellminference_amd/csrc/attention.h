@@ -36,6 +36,7 @@ struct AttnArgs {
     unsigned long long* stamps = nullptr;  // diagnostic (tools/attn_lab): per-workgroup s_memrealtime x4
     int cache_heads = 0;    // > 0: the cache holds cache_heads kv heads shared by every sequence (prefill lanes
                             // of one sequence): kv head kvh reads cache head kvh % cache_heads
+    int ppwg = 0;           // context positions per workgroup split (0: AttnGeom's PPWG; attn_stream.h sets it)
     int defer_merge = 0;    // != 0: only write the workgroup partials (plain stores); the splits are merged
                             // after the launch: 1 by the consumer (the wo GEMV's input staging, gemv.h
                             // XStageMerge), 2 by attn_merge_kernel (mha_launch launches it)
@@ -302,8 +303,8 @@ __device__ __forceinline__ void attn_merge(const float* part, float* out, int kv
 // Live split count of a kv head at position pos (workgroups that run attn_publish to the end).
 template <typename KT, int HD, int G>
 __device__ __forceinline__ int attn_live_splits(const AttnArgs<KT>& a, int kvh) {
-    constexpr int PPWG = AttnGeom<KT, HD>::PPWG;
-    return min(attn_pos(a, kvh) / PPWG + 1, a.max_splits);
+    const int ppwg = a.ppwg > 0 ? a.ppwg : AttnGeom<KT, HD>::PPWG;
+    return min(attn_pos(a, kvh) / ppwg + 1, a.max_splits);
 }
 
 // grid: n_kv_heads * wg_splits workgroups of 64 * WAVES threads

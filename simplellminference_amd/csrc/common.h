@@ -39,25 +39,48 @@ inline hipStream_t as_stream(sli_stream_t s) { return reinterpret_cast<hipStream
 // ---------------------------------------------------------------- device helpers
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
-    return v;
+// Lane exchanges inside a 16-lane DPP row as VALU operand modifiers (no LDS round trip, unlike the
+// ds_bpermute that __shfl_xor becomes): xor 1 and xor 2 as quad permutations, then the half-row mirror
+// (lane i <-> 7 - i: pairs each quad with the other quad of its 8) and the row mirror (i <-> 15 - i: pairs
+// the two halves). A butterfly over these four reaches every lane of the row; beyond 16 lanes the
+// exchange is a ds_bpermute (xor 16, xor 32).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
 }
+constexpr int kDppXor1 = 0xB1;        // quad_perm [1, 0, 3, 2]
+constexpr int kDppXor2 = 0x4E;        // quad_perm [2, 3, 0, 1]
+constexpr int kDppHalfMirror = 0x141;  // row_half_mirror
+constexpr int kDppMirror = 0x140;      // row_mirror
 
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
-    return v;
-}
-
-// sum over groups of `width` consecutive lanes (width a power of two <= 64)
+// sum over groups of `width` consecutive lanes (width a power of two <= 64); every lane of a group
+// gets the same value (each step adds the same two operands on both partners)
 template <int WIDTH>
 __device__ __forceinline__ float group_sum(float v) {
-#pragma unroll
-    for (int o = WIDTH / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
+    static_assert(WIDTH >= 1 && WIDTH <= 64 && (WIDTH & (WIDTH - 1)) == 0, "group width");
+    if constexpr (WIDTH >= 2) v += dpp_f<kDppXor1>(v);
+    if constexpr (WIDTH >= 4) v += dpp_f<kDppXor2>(v);
+    if constexpr (WIDTH >= 8) v += dpp_f<kDppHalfMirror>(v);
+    if constexpr (WIDTH >= 16) v += dpp_f<kDppMirror>(v);
+    if constexpr (WIDTH >= 32) v += __shfl_xor(v, 16, kWave);
+    if constexpr (WIDTH >= 64) v += __shfl_xor(v, 32, kWave);
     return v;
 }
+
+template <int WIDTH>
+__device__ __forceinline__ float group_max(float v) {
+    static_assert(WIDTH >= 1 && WIDTH <= 64 && (WIDTH & (WIDTH - 1)) == 0, "group width");
+    if constexpr (WIDTH >= 2) v = fmaxf(v, dpp_f<kDppXor1>(v));
+    if constexpr (WIDTH >= 4) v = fmaxf(v, dpp_f<kDppXor2>(v));
+    if constexpr (WIDTH >= 8) v = fmaxf(v, dpp_f<kDppHalfMirror>(v));
+    if constexpr (WIDTH >= 16) v = fmaxf(v, dpp_f<kDppMirror>(v));
+    if constexpr (WIDTH >= 32) v = fmaxf(v, __shfl_xor(v, 16, kWave));
+    if constexpr (WIDTH >= 64) v = fmaxf(v, __shfl_xor(v, 32, kWave));
+    return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) { return group_sum<64>(v); }
+__device__ __forceinline__ float wave_max(float v) { return group_max<64>(v); }
 
 // 16-byte loads. NT = non-temporal (streamed-once weights: MI355X_MICROARCH.md "nt-weights").
 template <bool NT>
