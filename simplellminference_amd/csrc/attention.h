@@ -144,8 +144,7 @@ __device__ __forceinline__ bool attn_publish(const AttnArgs<KT>& a, int kvh, int
         if constexpr (LATE_V) load_v();
 #pragma unroll
         for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int o = LPR; o < 64; o <<= 1) m[g] = fmaxf(m[g], __shfl_xor(m[g], o, kWave));
+            m[g] = stride_max<LPR>(m[g]);
 #pragma unroll
         for (int it = 0; it < kAttnNit; ++it) {
             float vf[EPV];
@@ -161,12 +160,9 @@ __device__ __forceinline__ bool attn_publish(const AttnArgs<KT>& a, int kvh, int
         // every lane of a row group holds the same p: reduce across row groups only
 #pragma unroll
         for (int g = 0; g < G; ++g) {
+            l[g] = stride_sum<LPR>(l[g]);
 #pragma unroll
-            for (int o = LPR; o < 64; o <<= 1) {
-                l[g] += __shfl_xor(l[g], o, kWave);
-#pragma unroll
-                for (int e = 0; e < EPV; ++e) ov[g][e] += __shfl_xor(ov[g][e], o, kWave);
-            }
+            for (int e = 0; e < EPV; ++e) ov[g][e] = stride_sum<LPR>(ov[g][e]);
         }
     }
     if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 4 + 1] = __builtin_amdgcn_s_memrealtime();

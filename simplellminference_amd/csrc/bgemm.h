@@ -252,9 +252,7 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
         }
     }
     if constexpr (NORM) {
-        ss += __shfl_xor(ss, 1, kWave);  // the 8 lanes of one sequence
-        ss += __shfl_xor(ss, 2, kWave);
-        ss += __shfl_xor(ss, 4, kWave);
+        ss = group_sum<8>(ss);  // the 8 lanes of one sequence
         if ((lane & 7) == 0) red[wave * 8 + sb] = ss;  // read after the stream's final barrier
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -274,7 +272,7 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
         if (c == cpt - 1) {  // tile j complete in every wave (uniform branch)
             float* Pb = P + (j & 1) * (kBgWaves * 128);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) acc[r] += __shfl_xor(acc[r], 8, kWave);  // hi + lo columns
+            for (int r = 0; r < 4; ++r) acc[r] += dpp_f<kDppRor8>(acc[r]);  // hi + lo columns (lane + 8)
             if ((lane & 8) == 0) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) Pb[wave * 128 + ((lane >> 4) * 4 + r) * 8 + (lane & 7)] = acc[r];

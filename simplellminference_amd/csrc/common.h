@@ -53,6 +53,40 @@ constexpr int kDppXor2 = 0x4E;        // quad_perm [2, 3, 0, 1]
 constexpr int kDppHalfMirror = 0x141;  // row_half_mirror
 constexpr int kDppMirror = 0x140;      // row_mirror
 
+constexpr int kDppRor8 = 0x128;        // row_ror:8 (lane i <- i + 8 mod 16: xor 8 inside a row)
+
+// Across rows: the gfx950 permlane swaps (VALU). With both operands the same value, permlane16_swap
+// returns {v with its odd rows replaced by the even rows, v with its even rows replaced by the odd
+// rows} and permlane32_swap the same for the two 32-lane halves, so the two results always hold a lane's
+// own value and its xor-16 (xor-32) partner's — in the same order on both partners.
+struct LanePair {
+    float a, b;
+};
+__device__ __forceinline__ LanePair lanes_xor16(float v) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return {__uint_as_float(r[0]), __uint_as_float(r[1])};
+}
+__device__ __forceinline__ LanePair lanes_xor32(float v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return {__uint_as_float(r[0]), __uint_as_float(r[1])};
+}
+__device__ __forceinline__ float sum_xor16(float v) {
+    const LanePair p = lanes_xor16(v);
+    return p.a + p.b;
+}
+__device__ __forceinline__ float sum_xor32(float v) {
+    const LanePair p = lanes_xor32(v);
+    return p.a + p.b;
+}
+__device__ __forceinline__ float max_xor16(float v) {
+    const LanePair p = lanes_xor16(v);
+    return fmaxf(p.a, p.b);
+}
+__device__ __forceinline__ float max_xor32(float v) {
+    const LanePair p = lanes_xor32(v);
+    return fmaxf(p.a, p.b);
+}
+
 // sum over groups of `width` consecutive lanes (width a power of two <= 64); every lane of a group
 // gets the same value (each step adds the same two operands on both partners)
 template <int WIDTH>
@@ -62,8 +96,8 @@ __device__ __forceinline__ float group_sum(float v) {
     if constexpr (WIDTH >= 4) v += dpp_f<kDppXor2>(v);
     if constexpr (WIDTH >= 8) v += dpp_f<kDppHalfMirror>(v);
     if constexpr (WIDTH >= 16) v += dpp_f<kDppMirror>(v);
-    if constexpr (WIDTH >= 32) v += __shfl_xor(v, 16, kWave);
-    if constexpr (WIDTH >= 64) v += __shfl_xor(v, 32, kWave);
+    if constexpr (WIDTH >= 32) v = sum_xor16(v);
+    if constexpr (WIDTH >= 64) v = sum_xor32(v);
     return v;
 }
 
@@ -74,8 +108,31 @@ __device__ __forceinline__ float group_max(float v) {
     if constexpr (WIDTH >= 4) v = fmaxf(v, dpp_f<kDppXor2>(v));
     if constexpr (WIDTH >= 8) v = fmaxf(v, dpp_f<kDppHalfMirror>(v));
     if constexpr (WIDTH >= 16) v = fmaxf(v, dpp_f<kDppMirror>(v));
-    if constexpr (WIDTH >= 32) v = fmaxf(v, __shfl_xor(v, 16, kWave));
-    if constexpr (WIDTH >= 64) v = fmaxf(v, __shfl_xor(v, 32, kWave));
+    if constexpr (WIDTH >= 32) v = max_xor16(v);
+    if constexpr (WIDTH >= 64) v = max_xor32(v);
+    return v;
+}
+
+// sum / max over the lanes congruent modulo STRIDE (the row groups of a wave that hold the same
+// columns: lanes STRIDE, 2·STRIDE, … apart); STRIDE in {4, 8, 16, 32, 64}. The xor-16/32 steps stay on
+// ds_bpermute here: in the attention tails (many independent values) the permlane swaps measured slower
+// (C4 GQA-4 attention 38.2 -> 43.8 us), the LDS pipe overlapping its round trips better.
+template <int STRIDE>
+__device__ __forceinline__ float stride_sum(float v) {
+    static_assert(STRIDE == 4 || STRIDE == 8 || STRIDE == 16 || STRIDE == 32 || STRIDE == 64, "stride");
+    if constexpr (STRIDE <= 4) v += __shfl_xor(v, 4, kWave);
+    if constexpr (STRIDE <= 8) v += dpp_f<kDppRor8>(v);
+    if constexpr (STRIDE <= 16) v += __shfl_xor(v, 16, kWave);
+    if constexpr (STRIDE <= 32) v += __shfl_xor(v, 32, kWave);
+    return v;
+}
+template <int STRIDE>
+__device__ __forceinline__ float stride_max(float v) {
+    static_assert(STRIDE == 4 || STRIDE == 8 || STRIDE == 16 || STRIDE == 32 || STRIDE == 64, "stride");
+    if constexpr (STRIDE <= 4) v = fmaxf(v, __shfl_xor(v, 4, kWave));
+    if constexpr (STRIDE <= 8) v = fmaxf(v, dpp_f<kDppRor8>(v));
+    if constexpr (STRIDE <= 16) v = fmaxf(v, __shfl_xor(v, 16, kWave));
+    if constexpr (STRIDE <= 32) v = fmaxf(v, __shfl_xor(v, 32, kWave));
     return v;
 }
 

@@ -731,8 +731,7 @@ __device__ __forceinline__ bool ps_attention(PsA& a, int l, int pos, float* smem
             }
 #pragma unroll
             for (int g = 0; g < G; ++g)
-#pragma unroll
-                for (int o = LPR; o < 64; o <<= 1) m[g] = fmaxf(m[g], __shfl_xor(m[g], o, kWave));
+                m[g] = stride_max<LPR>(m[g]);
 #pragma unroll
             for (int it = 0; it < NIT; ++it) {
                 float vf[EPV];
@@ -747,12 +746,9 @@ __device__ __forceinline__ bool ps_attention(PsA& a, int l, int pos, float* smem
             }
 #pragma unroll
             for (int g = 0; g < G; ++g) {
+                lsum[g] = stride_sum<LPR>(lsum[g]);
 #pragma unroll
-                for (int o = LPR; o < 64; o <<= 1) {
-                    lsum[g] += __shfl_xor(lsum[g], o, kWave);
-#pragma unroll
-                    for (int e = 0; e < EPV; ++e) ov[g][e] += __shfl_xor(ov[g][e], o, kWave);
-                }
+                for (int e = 0; e < EPV; ++e) ov[g][e] = stride_sum<LPR>(ov[g][e]);
             }
         }
         if (threadIdx.x == 64) ps_stamp(stamps, 2);  // wave 1's loads landed and scored
