@@ -204,6 +204,7 @@ def main():
         raise SystemExit(f"device error flag {st['error']}")
     wbytes, kvbytes = model.step_bytes()
     fam = model.time_families(a.gemv_iters)
+    sfl = model.time_stream(a.gemv_iters)  # the measured streaming-read floor of the same launches
     g = model.time_gemv(a.gemv_iters)
     if exec_mode == "persistent":
         # the step IS one kernel (ps_step_kernel): its algorithmic bytes (all weights + the live K/V) per launch
@@ -271,6 +272,10 @@ def main():
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "avg_launch_us": round(d["avg_us"], 3), "algorithmic_bytes_per_launch": round(d["bytes_per_launch"]),
+                     "stream_floor_us": round(sfl[dom], 3) if dom in sfl else None,
+                     "stream_floor_gbs": (round(d["bytes_per_launch"] / (sfl[dom] * 1e-6) / 1e9, 1)
+                                          if dom in sfl else None),
+                     "frac_of_stream": round(sfl[dom] / d["avg_us"], 4) if dom in sfl else None,
                      "launches_per_step": d["launches_per_step"],
                      "share_of_step_device_time": round(d["avg_us"] * d["launches_per_step"] / step_dev_us, 4),
                      "families_note": ("per-family timing of the launch path's kernels (the same arithmetic; "
@@ -281,7 +286,9 @@ def main():
                                       "launches_per_step": v["launches_per_step"],
                                       "gbs": round(v["bytes_per_launch"] / (v["avg_us"] * 1e-6) / 1e9, 1),
                                       "frac": round(v["bytes_per_launch"] / (v["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
-                                      "traffic": traffic_family.get(f)}
+                                      "traffic": traffic_family.get(f),
+                                      "stream_floor_us": round(sfl[f], 3),
+                                      "frac_of_stream": round(sfl[f] / v["avg_us"], 4)}
                                   for f, v in fam.items()},
                      "weight_streaming_average": {"avg_launch_us": round(g["avg_us"], 3),
                                                   "bytes_per_launch": round(g["bytes_per_launch"]),

@@ -110,7 +110,9 @@ int sli_add(const float* a, const float* b, float* out, int32_t n, sli_stream_t 
 
 /* kernel::emb_kernel_cuda (emb_kernel.cuh:6-7; CPU emb_kernel.cpp:4-21): out = table[token] (row
  * dequantised for SLI_DT_I8 with row_scale). token = token_dev ? *token_dev : token. Returns
- * SLI_ERR_RANGE for a host token outside [0, vocab); a device token outside that range writes zeros. */
+ * SLI_ERR_RANGE for a host token outside [0, vocab). A device token cannot be checked without a host
+ * sync: outside [0, vocab) it fills `out` with quiet NaNs, so the failure (the reference's LOG-exit,
+ * emb_kernel.cu:15-16) propagates loudly instead of as a plausible zero embedding. */
 int sli_embedding(int32_t token, const int32_t* token_dev, const void* table, int dtype, const float* row_scale,
                   float* out, int32_t vocab, int32_t dim, sli_stream_t stream);
 
@@ -266,6 +268,12 @@ int sli_model_time_steps(sli_model* m, int32_t iters, double* avg_us);
  * SLI_FAM_COUNT. */
 typedef enum { SLI_FAM_QKV = 0, SLI_FAM_ATTN, SLI_FAM_WO, SLI_FAM_GU, SLI_FAM_DOWN, SLI_FAM_LM, SLI_FAM_COUNT } sli_kernel_family;
 int sli_model_time_families(sli_model* m, int32_t iters, double* us, double* bytes, int32_t* launches);
+/* The measured streaming-read floor of the same launches: for each family, a pure read kernel (no
+ * arithmetic, 16-byte non-temporal loads, one 1024-thread workgroup per CU) over exactly the buffers that
+ * family's launches stream (each layer's weight matrix; K and V of the layer for attention, the
+ * allocated context), replayed the same way; us[f] = mean device µs per launch (the
+ * fraction of a measured stream-copy bandwidth). */
+int sli_model_time_stream(sli_model* m, int32_t iters, double* us);
 
 #ifdef __cplusplus
 }

@@ -110,6 +110,7 @@ _SIGS = {
     "sli_model_set_allreduce": (c_int, [c_vp, c_i32]),
     "sli_model_time_steps": (c_int, [c_vp, c_i32, P_d]),
     "sli_model_time_families": (c_int, [c_vp, c_i32, P_d, P_d, P_i32]),
+    "sli_model_time_stream": (c_int, [c_vp, c_i32, P_d]),
     "sli_tp_group_create": (c_int, [ctypes.POINTER(ModelConfig), c_i32, ctypes.POINTER(c_vp)]),
     "sli_tp_group_destroy": (c_int, [c_vp]),
     "sli_tp_group_rank": (c_int, [c_vp, c_i32, ctypes.POINTER(c_vp)]),

@@ -1762,6 +1762,83 @@ int sli_model_time_families(sli_model* m, int32_t iters, double* us, double* byt
     return rc;
 }
 
+namespace sli {
+// pure streaming read of up to two byte ranges (the stream floor of sli_model_time_stream): workgroup b
+// reads its contiguous 1/grid share of each range, 8 x 16 B per lane in flight
+__global__ void __launch_bounds__(1024) stream_read_kernel(const char* a, long long na, const char* b, long long nb,
+                                                           float* sink) {
+    float acc = 0.0f;
+    for (int r = 0; r < 2; ++r) {
+        const char* base = r ? b : a;
+        const long long n = r ? nb : na;
+        if (!base || n < 16) continue;
+        const long long per = (n / 16 + gridDim.x - 1) / gridDim.x;  // 16-B vectors per workgroup
+        const long long v0 = per * blockIdx.x, v1 = min(v0 + per, n / 16);
+        for (long long v = v0 + threadIdx.x; v < v1; v += 8 * 1024) {
+            u32x4 w[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) w[j] = load16<true>(base + min(v + j * 1024, v1 - 1) * 16);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc += __uint_as_float(w[j].x ^ w[j].w);
+        }
+    }
+    if (acc == 1.2345f) sink[threadIdx.x] = acc;  // never: keeps the loads
+}
+}  // namespace sli
+
+int sli_model_time_stream(sli_model* m, int32_t iters, double* us) {
+    SLI_CHECK(m && iters > 0 && us, SLI_ERR_ARG, "bad argument");
+    SLI_CHECK(!m->group, SLI_ERR_STATE, "time a group's ranks through a standalone model");
+    SLI_HIP(hipSetDevice(m->c.device));
+    struct Guard {
+        float* sink = nullptr;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        ~Guard() {
+            if (sink) (void)hipFree(sink);
+            if (e0) (void)hipEventDestroy(e0);
+            if (e1) (void)hipEventDestroy(e1);
+        }
+    } g;
+    SLI_HIP(hipMalloc(&g.sink, 4096));
+    SLI_HIP(hipEventCreate(&g.e0));
+    SLI_HIP(hipEventCreate(&g.e1));
+    const long long wb = m->wbytes, D = m->D, hd = m->hd;
+    const long long kvl = (long long)m->B * m->hkv * m->T * hd * m->kvbytes;  // one layer's K (or V)
+    const int grid = device_cus();
+    auto launch = [&](int f, int l) {
+        const char *a = nullptr, *b = nullptr;
+        long long na = 0, nb = 0;
+        const LayerW& w = m->layers[f == SLI_FAM_LM ? 0 : l];
+        switch (f) {
+            case SLI_FAM_QKV: a = (const char*)w.qkv; na = (m->hq + 2LL * m->hkv) * hd * D * wb; break;
+            case SLI_FAM_ATTN:
+                a = (const char*)m->kc + l * kvl;
+                b = (const char*)m->vc + l * kvl;
+                na = nb = kvl;
+                break;
+            case SLI_FAM_WO: a = (const char*)w.wo; na = D * m->hq * hd * wb; break;
+            case SLI_FAM_GU: a = (const char*)w.gu; na = 2LL * m->Il * D * wb; break;
+            case SLI_FAM_DOWN: a = (const char*)w.down; na = D * m->Il * wb; break;
+            default: a = (const char*)m->emb + (long long)m->v_lo * D * wb; na = (long long)m->v_n * D * wb; break;
+        }
+        hipLaunchKernelGGL(stream_read_kernel, dim3(grid), dim3(1024), 0, m->stream, a, na, b, nb, g.sink);
+    };
+    for (int f = 0; f < SLI_FAM_COUNT; ++f) {
+        const int n = f == SLI_FAM_LM ? 1 : m->L;
+        for (int l = 0; l < n; ++l) launch(f, l);  // warm-up
+        SLI_HIP(hipEventRecord(g.e0, m->stream));
+        for (int i = 0; i < iters; ++i)
+            for (int l = 0; l < n; ++l) launch(f, l);
+        SLI_HIP(hipEventRecord(g.e1, m->stream));
+        SLI_HIP(hipGetLastError());
+        float ms = 0.0f;
+        SLI_HIP(hipEventSynchronize(g.e1));
+        SLI_HIP(hipEventElapsedTime(&ms, g.e0, g.e1));
+        us[f] = 1000.0 * ms / ((double)iters * n);
+    }
+    return SLI_OK;
+}
+
 int sli_model_time_gemv(sli_model* m, int32_t iters, double* avg_us, double* bytes_per_launch,
                         int32_t* launches_per_step) {
     SLI_CHECK(m && iters > 0, SLI_ERR_ARG, "bad argument");

@@ -254,7 +254,7 @@ inline size_t gemv_res_floats(int units, int grid, int R) {
 // for the first weight chunk (staged 4-6 us into a 10-30 us launch). The epilogue (residual reads,
 // RoPE, K/V writes, logits) runs once per workgroup after the loop, one thread per unit.
 // Prologue order: input loads, first weight chunk, input commit + barrier (see XStage).
-template <typename WT, int R, int U, bool NT, class Epi, class Stage>
+template <typename WT, int R, int U, bool NT, class Epi, class Stage, int NB = 2>
 __device__ __forceinline__ void gemv_block(const WT* __restrict__ W, const GemvIn& in, Epi& epi, Stage& stage,
                                            float* smem) {
     const float* xs = smem + kGemvLdsHead;
@@ -325,37 +325,40 @@ __device__ __forceinline__ void gemv_block(const WT* __restrict__ W, const GemvI
         }
     };
 
-    // Two register buffers, both in flight before the input is committed. Every load is unconditional:
-    // a position past the wave's last step is clamped to that step, so the extra load duplicates one
-    // issued just before it (an in-flight miss to the same lines) and is never consumed; no clamped load
-    // is ever issued after its data was consumed (a fresh HBM round trip at the end of every wave).
-    u32x4 wa[U][R], wb[U][R];
+    // NB register buffers (steps), all in flight before the input is committed. Every load is
+    // unconditional: a position past the wave's last step is clamped to that step, so the extra load
+    // duplicates one issued just before it (an in-flight miss to the same lines) and is never consumed;
+    // no clamped load is ever issued after its data was consumed (a fresh HBM round trip at the end of
+    // every wave).
+    u32x4 wbuf[NB][U][R];
     int lu = u_begin, lc = 0;  // next step to load
     int cu = u_begin, cc = 0;  // next step to consume
-    load_step(lu, lc, wa);
-    next(lu, lc);
-    load_step(lu, lc, wb);
-    next(lu, lc);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        load_step(lu, lc, wbuf[b]);
+        next(lu, lc);
+    }
     __builtin_amdgcn_sched_barrier(0);
     stage.commit(smem, in);
     __syncthreads();
     epi.prefetch_b(pre_unit);
     t_staged = in.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
     int k = 0;
-    for (; k + 2 < nsteps; k += 2) {
-        consume_step(cu, cc, wa);
-        next(cu, cc);
-        load_step(lu, lc, wa);  // step k + 2
-        next(lu, lc);
-        consume_step(cu, cc, wb);
-        next(cu, cc);
-        load_step(lu, lc, wb);  // step k + 3, or a duplicate of k + 2
-        next(lu, lc);
+    for (; k + NB < nsteps; k += NB) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            consume_step(cu, cc, wbuf[b]);
+            next(cu, cc);
+            load_step(lu, lc, wbuf[b]);  // step k + b + NB, or a duplicate of the wave's last step
+            next(lu, lc);
+        }
     }
-    if (k < nsteps) {
-        consume_step(cu, cc, wa);
-        next(cu, cc);
-        if (k + 1 < nsteps) consume_step(cu, cc, wb);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        if (k + b < nsteps) {
+            consume_step(cu, cc, wbuf[b]);
+            next(cu, cc);
+        }
     }
     __syncthreads();
     for (int u = ub + (int)threadIdx.x; u < ue; u += kGemvThreads) {
@@ -375,12 +378,12 @@ __device__ __forceinline__ void gemv_block(const WT* __restrict__ W, const GemvI
     }
 }
 
-template <typename WT, int R, int U, bool NT, class Epi>
+template <typename WT, int R, int U, bool NT, class Epi, int NB = 2>
 __global__ void __launch_bounds__(kGemvThreads) gemv_kernel(const WT* __restrict__ W, GemvIn in, Epi epi_in) {
     Epi epi = epi_in;  // mutable per-thread copy (EpiLogits keeps a running key)
     extern __shared__ __attribute__((aligned(16))) float smem[];
     XStage<Vec16<WT>::N / 4> stage;
-    gemv_block<WT, R, U, NT>(W, in, epi, stage, smem);
+    gemv_block<WT, R, U, NT, Epi, XStage<Vec16<WT>::N / 4>, NB>(W, in, epi, stage, smem);
 }
 
 // the wo GEMV with its input merged from the attention's split partials (XStageMerge)
@@ -647,11 +650,11 @@ hipError_t launch_gemv_merge(const WT* W, const GemvIn& in, const Epi& epi, cons
     return hipGetLastError();
 }
 
-template <typename WT, int R, int U, bool NT, class Epi>
+template <typename WT, int R, int U, bool NT, class Epi, int NB = 2>
 hipError_t launch_gemv(const WT* W, const GemvIn& in, const Epi& epi, int units, hipStream_t s) {
     const int grid = gemv_blocks(units);
     const size_t lds = gemv_lds_bytes(in.cols) + sizeof(float) * gemv_res_floats(units, grid, R);
-    hipLaunchKernelGGL((gemv_kernel<WT, R, U, NT, Epi>), dim3(grid), dim3(kGemvThreads), lds, s, W, in, epi);
+    hipLaunchKernelGGL((gemv_kernel<WT, R, U, NT, Epi, NB>), dim3(grid), dim3(kGemvThreads), lds, s, W, in, epi);
     return hipGetLastError();
 }
 

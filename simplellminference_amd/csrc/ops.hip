@@ -115,7 +115,7 @@ __global__ void embedding_kernel(int token_host, const int32_t* token_dev, const
     const bool ok = token >= 0 && token < vocab;
     const float s = (ok && row_scale) ? row_scale[token] : 1.0f;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < dim; i += gridDim.x * blockDim.x)
-        out[i] = ok ? to_f32(table[(size_t)token * dim + i]) * s : 0.0f;
+        out[i] = ok ? to_f32(table[(size_t)token * dim + i]) * s : __int_as_float(0x7FC00000);  // poison: NaN
 }
 
 // ---------------------------------------------------------------- argmax (argmax.cpp:7-17)

@@ -304,6 +304,13 @@ class LlamaModel:
         return {f: {"avg_us": us[i], "bytes_per_launch": b[i], "launches_per_step": k[i]}
                 for i, f in enumerate(self.FAMILIES)}
 
+    def time_stream(self, iters: int = 20) -> dict:
+        """Per kernel family: mean device µs of a pure streaming read of the same buffers (the floor)."""
+        n = len(self.FAMILIES)
+        us = (ctypes.c_double * n)()
+        call("sli_model_time_stream", self._h, iters, us)
+        return {f: us[i] for i, f in enumerate(self.FAMILIES)}
+
     def time_gemv(self, iters: int = 20) -> dict:
         us, b, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int32()
         call("sli_model_time_gemv", self._h, iters, ctypes.byref(us), ctypes.byref(b), ctypes.byref(n))

@@ -167,6 +167,11 @@ def test_embedding(gpu, oracle, dtype):
         assert np.array_equal(got, oracle.embedding(tok, tab.astype(np.float32)))
     with pytest.raises(SliError):
         ops.embedding(512, _t(torch, tab))  # emb_kernel.cpp:10 rejects out-of-range tokens
+    for bad in (512, -1):  # a device token cannot be rejected before the launch: the row is poisoned (NaN)
+        got = ops.embedding(torch.tensor([bad], dtype=torch.int32, device="cuda"), _t(torch, tab)).cpu().numpy()
+        assert np.isnan(got).all()
+    got = ops.embedding(torch.tensor([17], dtype=torch.int32, device="cuda"), _t(torch, tab)).cpu().numpy()
+    assert np.array_equal(got, oracle.embedding(17, tab.astype(np.float32)))
 
 
 def test_argmax_first_max(gpu, oracle):

@@ -126,6 +126,12 @@ static void run_cfg(const __half* W, const GemvIn& in, float* y, int rows, hipSt
     CK((launch_gemv<__half, R, U, true>(W, in, e, (rows + R - 1) / R, s)));
 }
 
+template <int R, int U, int NB>
+static void run_cfg_nb(const __half* W, const GemvIn& in, float* y, int rows, hipStream_t s) {
+    EpiStore<R> e{y, nullptr, nullptr, 1.0f, rows};
+    CK((launch_gemv<__half, R, U, true, EpiStore<R>, NB>(W, in, e, (rows + R - 1) / R, s)));
+}
+
 static float time_graph(hipStream_t s, const std::function<void()>& body, int reps = 5) {
     hipGraph_t g;
     hipGraphExec_t ge;
@@ -198,11 +204,11 @@ int main(int argc, char** argv) {
         // int8 weights (the fp16 buffers reinterpreted: half their bytes), every (R, U) on each shape, and the
         // streaming-read ceiling of the same bytes
         using I8Run = std::function<void(const int8_t*, const GemvIn&, float*, int, hipStream_t)>;
-        auto mk = [](auto r_tag, auto u_tag) -> I8Run {
-            constexpr int R = decltype(r_tag)::value, U = decltype(u_tag)::value;
+        auto mk = [](auto r_tag, auto u_tag, auto nb_tag) -> I8Run {
+            constexpr int R = decltype(r_tag)::value, U = decltype(u_tag)::value, NB = decltype(nb_tag)::value;
             return [](const int8_t* W, const GemvIn& in, float* y, int rows, hipStream_t s) {
                 EpiStore<R> e{y, nullptr, nullptr, 1.0f, rows};
-                CK((launch_gemv<int8_t, R, U, true>(W, in, e, (rows + R - 1) / R, s)));
+                CK((launch_gemv<int8_t, R, U, true, EpiStore<R>, NB>(W, in, e, (rows + R - 1) / R, s)));
             };
         };
         using I1 = std::integral_constant<int, 1>;
@@ -210,9 +216,10 @@ int main(int argc, char** argv) {
         using I3 = std::integral_constant<int, 3>;
         using I4 = std::integral_constant<int, 4>;
         std::vector<std::pair<const char*, I8Run>> cf = {
-            {"R1U1", mk(I1{}, I1{})}, {"R1U2", mk(I1{}, I2{})}, {"R1U3", mk(I1{}, I3{})}, {"R1U4", mk(I1{}, I4{})},
-            {"R2U1", mk(I2{}, I1{})}, {"R2U2", mk(I2{}, I2{})}, {"R2U3", mk(I2{}, I3{})}, {"R4U1", mk(I4{}, I1{})},
-            {"R4U2", mk(I4{}, I2{})}};
+            {"R1U2", mk(I1{}, I2{}, I2{})}, {"R1U2NB3", mk(I1{}, I2{}, I3{})}, {"R1U2NB4", mk(I1{}, I2{}, I4{})},
+            {"R1U4", mk(I1{}, I4{}, I2{})}, {"R1U4NB3", mk(I1{}, I4{}, I3{})},
+            {"R2U2", mk(I2{}, I2{}, I2{})}, {"R2U2NB3", mk(I2{}, I2{}, I3{})}, {"R2U2NB4", mk(I2{}, I2{}, I4{})},
+            {"R2U1NB4", mk(I2{}, I1{}, I4{})}};
         for (int si = 0; si < 4; ++si) {
             const Shape& sh = kShapes[si];
             const double bytes = (double)sh.rows * sh.cols;
@@ -263,6 +270,33 @@ int main(int argc, char** argv) {
                 fwrite(hdr, 4, 3, f);
                 fwrite(h.data(), 8, h.size(), f);
             }
+        }
+        // the int8 engine configurations (half the bytes: the fp16 buffers reinterpreted)
+        for (int si : {0, 1, 2, 3}) {
+            const Shape& sh = kShapes[si];
+            const int R = (si == 0 || si == 2) ? 2 : 1;
+            CK(hipMemset(st, 0, (size_t)NL * nst * 8));
+            time_graph(s, [&] {
+                for (int l = 0; l < NL; ++l) {
+                    GemvIn in = in_for0(si);
+                    in.stamps = st + (size_t)l * nst;
+                    const int8_t* W8 = (const int8_t*)w[si][l];
+                    if (R == 2) {
+                        EpiStore<2> e{y, nullptr, nullptr, 1.0f, sh.rows};
+                        CK((launch_gemv<int8_t, 2, 2, true>(W8, in, e, sh.rows / 2, s)));
+                    } else if (si == 1) {
+                        EpiStore<1> e{y, nullptr, nullptr, 1.0f, sh.rows};
+                        CK((launch_gemv<int8_t, 1, 2, true>(W8, in, e, sh.rows, s)));
+                    } else {
+                        EpiStore<1> e{y, nullptr, nullptr, 1.0f, sh.rows};
+                        CK((launch_gemv<int8_t, 1, 4, true>(W8, in, e, sh.rows, s)));
+                    }
+                }
+            }, 1);
+            CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+            const int hdr[3] = {si + 100, R, NL};  // si + 100: int8
+            fwrite(hdr, 4, 3, f);
+            fwrite(h.data(), 8, h.size(), f);
         }
         fclose(f);
         printf("wrote stamps\n");
@@ -377,9 +411,9 @@ int main(int argc, char** argv) {
         return 0;
     }
     std::vector<Cfg> cfgs = {
-        {"R2U4", run_cfg<2, 4, true>}, {"R1U8", run_cfg<1, 8, true>}, {"R1U4", run_cfg<1, 4, true>},
-        {"R4U2", run_cfg<4, 2, true>}, {"R2U2", run_cfg<2, 2, true>}, {"R1U2", run_cfg<1, 2, true>},
-        {"R1U6", run_cfg<1, 6, true>},
+        {"R2U4", run_cfg<2, 4, true>}, {"R2U4NB3", run_cfg_nb<2, 4, 3>}, {"R2U2NB4", run_cfg_nb<2, 2, 4>},
+        {"R1U6", run_cfg<1, 6, true>}, {"R1U6NB3", run_cfg_nb<1, 6, 3>}, {"R1U4NB3", run_cfg_nb<1, 4, 3>},
+        {"R1U2", run_cfg<1, 2, true>}, {"R1U2NB3", run_cfg_nb<1, 2, 3>}, {"R1U2NB4", run_cfg_nb<1, 2, 4>},
     };
     auto in_for = [&](int si) { return GemvIn{x, si == 3 ? nullptr : nw, 1e-5f, kShapes[si].cols}; };
 

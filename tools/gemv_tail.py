@@ -31,7 +31,8 @@ def main(path):
         steps = st[:, :, 3] & 0xFFFFFFFF
         xcd = (st[:, :, 3] >> 32) & 15
         pc = lambda a, q: float(np.percentile(a[live], q))
-        print(f"{NAMES[si]:5s} R{r}: entry p50 {pc(ent,50):5.2f} p99 {pc(ent,99):5.2f} max {pc(ent,100):5.2f} | "
+        name = NAMES[si % 100] + ("-i8" if si >= 100 else "")
+        print(f"{name:8s} R{r}: entry p50 {pc(ent,50):5.2f} p99 {pc(ent,99):5.2f} max {pc(ent,100):5.2f} | "
               f"staged p50 {pc(stg,50):5.2f} p99 {pc(stg,99):5.2f} | exit p10 {pc(ex,10):5.2f} p50 {pc(ex,50):5.2f} "
               f"p90 {pc(ex,90):5.2f} p99 {pc(ex,99):5.2f} max {pc(ex,100):5.2f} us")
         print("      exit mean by XCD: " + " ".join(f"{x}:{ex[live & (xcd == x)].mean():5.2f}" for x in range(8)))
