@@ -1,7 +1,7 @@
 """Per-rank decode-step time of one tensor-parallel shard on ONE GPU, without a communicator
 (SLI_DEBUG_NOCOMM: the rank's kernels at their real shapes, no RCCL all-reduces; values are not a model).
 Estimates the compute part of config C2 (Llama-2-7B at TP N); the collectives come on top.
-    python tools/tp_rank_time.py [N ...]
+    python tools/tp_rank_time.py [N ...]            (TP_EXEC=persistent: the one-launch step instead)
 """
 import os
 import sys
@@ -17,6 +17,11 @@ for world in [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]:
     m = LlamaModel(config=preset("llama2-7b"), w_dtype="f16", kv_dtype="f16", seed=1, tp_rank=world - 1,
                    tp_size=world).init()
     m.fill_kv_synthetic(7, 2047)
+    if os.environ.get("TP_EXEC"):
+        try:
+            m.set_exec(os.environ["TP_EXEC"])
+        except Exception as e:  # noqa: BLE001 - report and go on with the launch graph
+            print(f"tp{world}: {os.environ['TP_EXEC']} refused ({e})", flush=True)
     m.set_state(1234, 2047, advance=False)
     for _ in range(10):
         m.step()
@@ -27,5 +32,6 @@ for world in [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]:
         m.step()
     m.sync()
     ms = 1e3 * (time.perf_counter() - t0) / n
-    print(f"tp{world} rank {world - 1}: {ms:.3f} ms/step compute (no all-reduces)", flush=True)
+    print(f"tp{world} rank {world - 1} [{m.exec_mode()}]: {ms:.3f} ms/step compute (no all-reduces)", flush=True)
+    m.close()
     m.close()
