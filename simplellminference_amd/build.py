@@ -40,48 +40,56 @@ def _headers() -> list[str]:
     return hs
 
 
-def _obj(src: str) -> str:
+def _obj(src: str, build_dir: str = BUILD) -> str:
     rel = os.path.relpath(src, CSRC).replace(os.sep, "__")
-    return os.path.join(BUILD, rel + ".o")
+    return os.path.join(build_dir, rel + ".o")
 
 
-def _compile(src: str, force: bool) -> str:
-    obj = _obj(src)
+def _compile(src: str, force: bool, build_dir: str = BUILD, defines: tuple = ()) -> str:
+    obj = _obj(src, build_dir)
     newest_dep = max([os.path.getmtime(src)] + [os.path.getmtime(h) for h in _headers()])
     if not force and os.path.exists(obj) and os.path.getmtime(obj) >= newest_dep:
         return obj
     lang = ["-x", "hip"] if src.endswith(".cpp") else []
-    cmd = ["hipcc", *lang, *CXXFLAGS, "-c", src, "-o", obj]
+    cmd = ["hipcc", *lang, *CXXFLAGS, *[f"-D{d}" for d in defines], "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
     return obj
 
 
-def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -> str:
-    os.makedirs(BUILD, exist_ok=True)
+def build(force: bool = False, jobs: int | None = None, verbose: bool = False, variant: str | None = None,
+          defines: tuple = ()) -> str:
+    """variant: an A/B experiment build (tools/ab_variants.sh) — objects in _build_variants/<variant>, the
+    library as libsli_<variant>.so beside libsli.so (loaded with SLI_LIB_VARIANT=<variant>), compiled
+    with the extra -D defines."""
+    build_dir = BUILD if variant is None else os.path.join(PKG, "_build_variants", variant)
+    lib = LIB if variant is None else os.path.join(PKG, f"libsli_{variant}.so")
+    os.makedirs(build_dir, exist_ok=True)
     srcs = sources()
     jobs = jobs or min(8, len(srcs), os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, force), srcs))
+        objs = list(ex.map(lambda s: _compile(s, force or variant is not None, build_dir, tuple(defines)), srcs))
     newest = max(os.path.getmtime(o) for o in objs)
-    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < newest:
-        cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs,
+    if force or variant is not None or not os.path.exists(lib) or os.path.getmtime(lib) < newest:
+        cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *objs,
                "-L", os.path.join(ROCM, "lib"), "-lrccl", f"-Wl,-rpath,{os.path.join(ROCM, 'lib')}"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
     if verbose:
-        print(f"built {LIB}")
-    return LIB
+        print(f"built {lib}")
+    return lib
 
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--jobs", type=int, default=None)
+    ap.add_argument("--variant", default=None, help="A/B build: libsli_<variant>.so")
+    ap.add_argument("-D", dest="defines", action="append", default=[], help="extra define for a variant build")
     a = ap.parse_args(argv)
-    build(force=a.force, jobs=a.jobs, verbose=True)
+    build(force=a.force, jobs=a.jobs, verbose=True, variant=a.variant, defines=tuple(a.defines))
     return 0
 
 

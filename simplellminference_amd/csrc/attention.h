@@ -67,8 +67,14 @@ struct AttnGeom {
 
 // tools/attn_lab (profiles/r03_attn_lab.txt): MHA / GQA-2 16 waves, GQA-4 8, GQA-8 4; V loaded after the
 // scores (K and V never live together) up to GQA-4.
-__host__ __device__ constexpr int attn_waves(int g) { return g <= 2 ? 16 : g == 4 ? 8 : 4; }
-__host__ __device__ constexpr bool attn_late_v(int g) { return g <= 4; }
+#ifndef SLI_ATTN_WAVES_MHA
+#define SLI_ATTN_WAVES_MHA 16
+#endif
+#ifndef SLI_ATTN_LATE_V_MHA
+#define SLI_ATTN_LATE_V_MHA 1
+#endif
+__host__ __device__ constexpr int attn_waves(int g) { return g == 1 ? SLI_ATTN_WAVES_MHA : g <= 2 ? 16 : g == 4 ? 8 : 4; }
+__host__ __device__ constexpr bool attn_late_v(int g) { return g == 1 ? SLI_ATTN_LATE_V_MHA != 0 : g <= 4; }
 
 // grid: n_kv_heads * wg_splits workgroups; wave w of workgroup (kvh, s) owns the w-th slice of split s.
 // The WAVES slice states are merged in LDS, so one partial per (q head, workgroup) reaches the workspace.
