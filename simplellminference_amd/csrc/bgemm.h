@@ -40,6 +40,10 @@ constexpr int kBgFlagOff = 704;
 constexpr int kBgPBytes = 2 * kBgWaves * 16 * 8 * 4;  // double-buffered per-wave tile partials
 constexpr int kBgLdsMax = 160 * 1024;
 constexpr int kBgU = 4;                // 16-byte weight loads per lane per step (two steps in flight)
+#ifndef SLI_BG_NORM_SPLIT
+#define SLI_BG_NORM_SPLIT 0
+#endif
+constexpr bool kBgNormSplit = SLI_BG_NORM_SPLIT;  // fused-RMS plans may split k (sums of squares merged)
 
 struct BgIn {
     const float* x;       // [B][K] fp32 activations
@@ -77,7 +81,9 @@ inline BgPlan bg_plan(int ntiles, int K, int B, bool norm, int cus = 256) {
     double best_cost = 1e30;
     for (int s = 1; s <= 16; ++s) {
         if (s > 1 && nkb / s < kBgWaves) break;  // every wave keeps at least one block per tile
-        if (norm && s > 1) break;  // the fused RMS needs the whole row in one workgroup (bgemm_kernel)
+        // fused RMS over several splits: each split's sum of squares travels with its partials and the
+        // group's last arriver normalises the merged sums (bgemm_kernel)
+        if (norm && s > 1 && !kBgNormSplit) break;
         const int kbs = (nkb + s - 1) / s;
         if (kbs * 32 > kBgMaxStageK) continue;  // staging registers
         for (int tpw = 1; tpw <= 64; ++tpw) {
@@ -86,7 +92,7 @@ inline BgPlan bg_plan(int ntiles, int K, int B, bool norm, int cus = 256) {
             const int wgs = groups * s;
             const int rounds = (wgs + cus - 1) / cus;
             double per_wg = (double)tpw * kbs + 0.25 * kbs * B / 8.0 + 40.0;
-            if (norm) per_wg += 0.25 * nkb * B / 8.0;
+            if (norm) per_wg += s > 1 ? 0.05 * kbs : 0.25 * nkb * B / 8.0;
             if (s > 1) per_wg += 20.0 + 0.5 * s * tpw;
             const double cost = rounds * per_wg;
             if (cost < best_cost - 1e-9) {
@@ -104,8 +110,12 @@ inline BgPlan bg_plan(int ntiles, int K, int B, bool norm, int cus = 256) {
 }
 
 // device workspace of a plan: split partials (256-B aligned), then one arrival counter per group
+// (the partials are followed by the fused RMS's per-split sums of squares, [groups][splits][8])
 inline size_t bg_part_bytes(const BgPlan& p) {
-    return p.splits > 1 ? (((size_t)p.ntiles * p.splits * 128 * sizeof(float) + 255) & ~(size_t)255) : 0;
+    return p.splits > 1
+               ? ((((size_t)p.ntiles * p.splits * 128 + (size_t)p.groups * p.splits * 8) * sizeof(float) + 255) &
+                  ~(size_t)255)
+               : 0;
 }
 inline size_t bg_ws_bytes(const BgPlan& p) { return bg_part_bytes(p) + sizeof(unsigned) * (size_t)p.groups + 256; }
 
@@ -262,13 +272,16 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
     // ---- 5. stream the tiles
     bg_float4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
     const u32x4* wimg = img + (size_t)(wb0 - kb0) * 64 + lane;
-    auto consume = [&](int k, const u32x4(&w)[kBgU]) {
-        const int j = k / cpt, c = k - j * cpt;
+    auto mfma_step = [&](int k, const u32x4(&w)[kBgU]) {
+        const int c = k - (k / cpt) * cpt;
 #pragma unroll
         for (int u = 0; u < kBgU; ++u) {
             const int r = c * kBgU + u;
             if (r < wnb) acc = bg_mfma(w[u], wimg[(size_t)r * 64], acc);
         }
+    };
+    auto tile_end = [&](int k) {
+        const int j = k / cpt, c = k - j * cpt;
         if (c == cpt - 1) {  // tile j complete in every wave (uniform branch)
             float* Pb = P + (j & 1) * (kBgWaves * 128);
 #pragma unroll
@@ -293,22 +306,36 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
         }
     };
     int k = 0;
+    // The next step's loads go out as soon as the current step's MFMAs have read their registers, BEFORE
+    // the tile-end workgroup barrier: two steps stay in flight through every tile boundary.
     for (; k + 2 < nsteps; k += 2) {
-        consume(k, wa);
+        mfma_step(k, wa);
         load_step(k + 2, wa);
-        consume(k + 1, wb);
+        tile_end(k);
+        mfma_step(k + 1, wb);
         load_step(k + 3, wb);
+        tile_end(k + 1);
     }
-    if (k < nsteps) consume(k, wa);
-    if (k + 1 < nsteps) consume(k + 1, wb);
+    if (k < nsteps) {
+        mfma_step(k, wa);
+        tile_end(k);
+    }
+    if (k + 1 < nsteps) {
+        mfma_step(k + 1, wb);
+        tile_end(k + 1);
+    }
     __syncthreads();
     if constexpr (NORM) {  // per-sequence 1/rms from the waves' sums of squares, in wave order
         if (tid < B) {
             float t = 0.0f;
             for (int w = 0; w < kBgWaves; ++w) t += red[w * 8 + tid];
-            const float tep = t / (float)K;         // rms_kernel.cpp:17
-            const float rms = sqrtf(tep + in.eps);  // :18
-            inv[tid] = 1.0f / rms;                  // :19
+            if (S == 1) {
+                const float tep = t / (float)K;         // rms_kernel.cpp:17
+                const float rms = sqrtf(tep + in.eps);  // :18
+                inv[tid] = 1.0f / rms;                  // :19
+            } else {
+                inv[tid] = t;  // this split's sum of squares: published with the partials
+            }
         }
         __syncthreads();
     }
@@ -333,6 +360,10 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
             __hip_atomic_store(in.ws + ((size_t)(t0 + j) * S + s) * 128 + r, R[e], __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
+        float* ssw = in.ws + (size_t)in.ntiles * S * 128 + (size_t)g * S * 8;  // [splits][8] of this group
+        if constexpr (NORM) {
+            if (tid < B) __hip_atomic_store(ssw + s * 8 + tid, inv[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before the arrival
         __syncthreads();
         if (tid == 0) {
@@ -342,6 +373,17 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
         }
         __syncthreads();
         if (*flag == 0) return;  // uniform
+        if constexpr (NORM) {  // the whole row's sum of squares: the splits' sums in split order
+            if (tid < B) {
+                float t = 0.0f;
+                for (int sp = 0; sp < S; ++sp)
+                    t += bg_load_sc1(ssw, (unsigned)(sizeof(float) * S * 8), 4u * (unsigned)(sp * 8 + tid));
+                const float tep = t / (float)K;         // rms_kernel.cpp:17
+                const float rms = sqrtf(tep + in.eps);  // :18
+                inv[tid] = 1.0f / rms;                  // :19
+            }
+            __syncthreads();
+        }
         const float* base = in.ws + (size_t)t0 * S * 128;
         const unsigned bytes = (unsigned)(sizeof(float) * (size_t)ntg * S * 128);
         for (int it = tid; it < items; it += kBgThreads) {
@@ -352,6 +394,10 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
                 const unsigned o = (unsigned)((j * S + sp) * 128);
                 v0 += bg_load_sc1(base, bytes, 4u * (o + i * 8 + b));
                 v1 += bg_load_sc1(base, bytes, 4u * (o + (i + 8) * 8 + b));
+            }
+            if constexpr (NORM) {
+                v0 *= inv[b];
+                v1 *= inv[b];
             }
             epi.store(t0 + j, i, b, v0, v1, keys);
         }

@@ -30,10 +30,6 @@ inline size_t gemv_lds_bytes(int cols) { return sizeof(float) * (size_t)(kGemvLd
 
 constexpr int kGemvStageV4 = 4;  // float4 of x per thread: 1024 threads x 4 x 4 = 16384 columns
 
-#ifndef SLI_GEMV_SPREAD
-#define SLI_GEMV_SPREAD 0
-#endif
-
 // The prologue is split into issue (global loads into registers) and commit (normalise, write LDS) so
 // the kernel can issue its input loads FIRST, its weight loads second, and wait only for the input:
 // s_waitcnt vmcnt counts in issue order, so an input load issued after the weights would wait for the
@@ -62,20 +58,9 @@ struct XStage {
         const float4* w4 = reinterpret_cast<const float4*>(in.norm_w ? in.norm_w : in.x);
 #pragma unroll
         for (int k = 0; k < kGemvStageV4; ++k) {
-            xr[k] = x4[sidx(tid + k * nt, n4)];
-            wr[k] = w4[sidx(tid + k * nt, n4)];
+            xr[k] = x4[min(tid + k * nt, n4 - 1)];
+            wr[k] = w4[min(tid + k * nt, n4 - 1)];
         }
-    }
-    // Index of staging round j >= n4 (a duplicate load/store): wrapped back into the vector, so each
-    // duplicate hits a line its wave reads anyway. Clamping every duplicate to the LAST float4 instead
-    // sent 3/4 of all staging requests of every CU (cols 4096: rounds 1-3 of 1024 threads) to one
-    // 16-byte address — one L2 channel of every XCD serving ~1500 requests ahead of the real input.
-    __device__ __forceinline__ static int sidx(int j, int n4) {
-#if SLI_GEMV_SPREAD
-        return j < n4 ? j : j % n4;
-#else
-        return min(j, n4 - 1);
-#endif
     }
     // x (optionally RMS-normalised, rms_kernel.cpp:5-23) into LDS; the caller then barriers. Stores are
     // unconditional too (clamped rounds rewrite the last vector with its own value).
@@ -85,7 +70,7 @@ struct XStage {
         const int tid = threadIdx.x, nt = kGemvThreads, n4 = in.cols >> 2;
         if (in.norm_w == nullptr) {
 #pragma unroll
-            for (int k = 0; k < kGemvStageV4; ++k) xs4[xswz<G>(sidx(tid + k * nt, n4))] = xr[k];
+            for (int k = 0; k < kGemvStageV4; ++k) xs4[xswz<G>(min(tid + k * nt, n4 - 1))] = xr[k];
             return;
         }
         float ss = 0.0f;
@@ -116,7 +101,7 @@ struct XStage {
             o.y = (xr[k].y * inv) * wr[k].y;
             o.z = (xr[k].z * inv) * wr[k].z;
             o.w = (xr[k].w * inv) * wr[k].w;
-            xs4[xswz<G>(sidx(tid + k * nt, n4))] = o;
+            xs4[xswz<G>(min(tid + k * nt, n4 - 1))] = o;
         }
     }
 };
@@ -499,19 +484,11 @@ struct EpiQKV {
         pre_pos = *pos_dev;
         int r[2];
         rows(u, r);
-#if SLI_GEMV_SPREAD
-        // grid-uniform branch, before the weight loads: no per-thread load of one shared address
-        if (rscale) {
-            pre_s0 = rscale[r[0]];
-            pre_s1 = rscale[r[1]];
-        }
-#else
         // without row scales: an unconditional load of a known-valid element (sin_t[0]), never a row
         // index into the [T][hd/2] table
         const float* sp = rscale ? rscale : sin_t;
         pre_s0 = sp[rscale ? r[0] : 0];
         pre_s1 = sp[rscale ? r[1] : 0];
-#endif
     }
     // after the input commit (the position has landed with the input): the table row of this position
     __device__ void prefetch_b(int u) {
@@ -576,15 +553,9 @@ struct EpiSwiGLU {
     }
     __device__ void prefetch_a(int u) {
         pre_u = u;
-#if SLI_GEMV_SPREAD
-        // without row scales: a valid element of the thread's own unit (act[u]), not one address for all
-        pre_s0 = (rscale ? rscale : act)[u];
-        pre_s1 = (rscale ? rscale + inter : act)[u];
-#else
         const float* sp = rscale ? rscale : act;
         pre_s0 = sp[rscale ? u : 0];
         pre_s1 = sp[rscale ? inter + u : 0];
-#endif
     }
     __device__ void prefetch_b(int) {}
     __device__ void store(int u, const int* r, const float* acc) const {
