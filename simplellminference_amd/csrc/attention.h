@@ -66,12 +66,13 @@ struct AttnGeom {
 };
 
 // tools/attn_lab (profiles/r03_attn_lab.txt): MHA / GQA-2 16 waves, GQA-4 8, GQA-8 4; V loaded after the
-// scores (K and V never live together) up to GQA-4.
+// scores (K and V never live together) for GQA-2 and GQA-4. MHA (57 VGPRs either way) issues K and V
+// together: C1 attention 9.17 -> 8.92 us in the step (round 2, tools/ab_variants.sh).
 #ifndef SLI_ATTN_WAVES_MHA
 #define SLI_ATTN_WAVES_MHA 16
 #endif
 #ifndef SLI_ATTN_LATE_V_MHA
-#define SLI_ATTN_LATE_V_MHA 1
+#define SLI_ATTN_LATE_V_MHA 0
 #endif
 __host__ __device__ constexpr int attn_waves(int g) { return g == 1 ? SLI_ATTN_WAVES_MHA : g <= 2 ? 16 : g == 4 ? 8 : 4; }
 __host__ __device__ constexpr bool attn_late_v(int g) { return g == 1 ? SLI_ATTN_LATE_V_MHA != 0 : g <= 4; }

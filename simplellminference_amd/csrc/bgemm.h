@@ -40,10 +40,6 @@ constexpr int kBgFlagOff = 704;
 constexpr int kBgPBytes = 2 * kBgWaves * 16 * 8 * 4;  // double-buffered per-wave tile partials
 constexpr int kBgLdsMax = 160 * 1024;
 constexpr int kBgU = 4;                // 16-byte weight loads per lane per step (two steps in flight)
-#ifndef SLI_BG_NORM_SPLIT
-#define SLI_BG_NORM_SPLIT 0
-#endif
-constexpr bool kBgNormSplit = SLI_BG_NORM_SPLIT;  // fused-RMS plans may split k (sums of squares merged)
 
 struct BgIn {
     const float* x;       // [B][K] fp32 activations
@@ -81,9 +77,10 @@ inline BgPlan bg_plan(int ntiles, int K, int B, bool norm, int cus = 256) {
     double best_cost = 1e30;
     for (int s = 1; s <= 16; ++s) {
         if (s > 1 && nkb / s < kBgWaves) break;  // every wave keeps at least one block per tile
-        // fused RMS over several splits: each split's sum of squares travels with its partials and the
-        // group's last arriver normalises the merged sums (bgemm_kernel)
-        if (norm && s > 1 && !kBgNormSplit) break;
+        // the fused RMS needs the whole row in one workgroup (measured round 2: splitting k for the fused-
+        // RMS plans, each split's sum of squares merged by the last arriver, was correct but slower — at
+        // K 4096 a split leaves each wave one partly-filled step per tile and a barrier per step)
+        if (norm && s > 1) break;
         const int kbs = (nkb + s - 1) / s;
         if (kbs * 32 > kBgMaxStageK) continue;  // staging registers
         for (int tpw = 1; tpw <= 64; ++tpw) {
@@ -92,7 +89,7 @@ inline BgPlan bg_plan(int ntiles, int K, int B, bool norm, int cus = 256) {
             const int wgs = groups * s;
             const int rounds = (wgs + cus - 1) / cus;
             double per_wg = (double)tpw * kbs + 0.25 * kbs * B / 8.0 + 40.0;
-            if (norm) per_wg += s > 1 ? 0.05 * kbs : 0.25 * nkb * B / 8.0;
+            if (norm) per_wg += 0.25 * nkb * B / 8.0;
             if (s > 1) per_wg += 20.0 + 0.5 * s * tpw;
             const double cost = rounds * per_wg;
             if (cost < best_cost - 1e-9) {
@@ -110,12 +107,8 @@ inline BgPlan bg_plan(int ntiles, int K, int B, bool norm, int cus = 256) {
 }
 
 // device workspace of a plan: split partials (256-B aligned), then one arrival counter per group
-// (the partials are followed by the fused RMS's per-split sums of squares, [groups][splits][8])
 inline size_t bg_part_bytes(const BgPlan& p) {
-    return p.splits > 1
-               ? ((((size_t)p.ntiles * p.splits * 128 + (size_t)p.groups * p.splits * 8) * sizeof(float) + 255) &
-                  ~(size_t)255)
-               : 0;
+    return p.splits > 1 ? (((size_t)p.ntiles * p.splits * 128 * sizeof(float) + 255) & ~(size_t)255) : 0;
 }
 inline size_t bg_ws_bytes(const BgPlan& p) { return bg_part_bytes(p) + sizeof(unsigned) * (size_t)p.groups + 256; }
 
@@ -231,7 +224,7 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
             w[u] = load16<true>(base + (size_t)bi * 64);
         }
     };
-    u32x4 wa[kBgU], wb[kBgU];
+    u32x4 wa[kBgU], wb[kBgU];  // (a third step in flight measured slower: C4 1660 -> 1546 tok/s)
     load_step(0, wa);
     load_step(1, wb);
     __builtin_amdgcn_sched_barrier(0);
@@ -329,13 +322,9 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
         if (tid < B) {
             float t = 0.0f;
             for (int w = 0; w < kBgWaves; ++w) t += red[w * 8 + tid];
-            if (S == 1) {
-                const float tep = t / (float)K;         // rms_kernel.cpp:17
-                const float rms = sqrtf(tep + in.eps);  // :18
-                inv[tid] = 1.0f / rms;                  // :19
-            } else {
-                inv[tid] = t;  // this split's sum of squares: published with the partials
-            }
+            const float tep = t / (float)K;         // rms_kernel.cpp:17
+            const float rms = sqrtf(tep + in.eps);  // :18
+            inv[tid] = 1.0f / rms;                  // :19
         }
         __syncthreads();
     }
@@ -360,10 +349,6 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
             __hip_atomic_store(in.ws + ((size_t)(t0 + j) * S + s) * 128 + r, R[e], __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
-        float* ssw = in.ws + (size_t)in.ntiles * S * 128 + (size_t)g * S * 8;  // [splits][8] of this group
-        if constexpr (NORM) {
-            if (tid < B) __hip_atomic_store(ssw + s * 8 + tid, inv[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before the arrival
         __syncthreads();
         if (tid == 0) {
@@ -373,17 +358,6 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
         }
         __syncthreads();
         if (*flag == 0) return;  // uniform
-        if constexpr (NORM) {  // the whole row's sum of squares: the splits' sums in split order
-            if (tid < B) {
-                float t = 0.0f;
-                for (int sp = 0; sp < S; ++sp)
-                    t += bg_load_sc1(ssw, (unsigned)(sizeof(float) * S * 8), 4u * (unsigned)(sp * 8 + tid));
-                const float tep = t / (float)K;         // rms_kernel.cpp:17
-                const float rms = sqrtf(tep + in.eps);  // :18
-                inv[tid] = 1.0f / rms;                  // :19
-            }
-            __syncthreads();
-        }
         const float* base = in.ws + (size_t)t0 * S * 128;
         const unsigned bytes = (unsigned)(sizeof(float) * (size_t)ntg * S * 128);
         for (int it = tid; it < items; it += kBgThreads) {
@@ -394,10 +368,6 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
                 const unsigned o = (unsigned)((j * S + sp) * 128);
                 v0 += bg_load_sc1(base, bytes, 4u * (o + i * 8 + b));
                 v1 += bg_load_sc1(base, bytes, 4u * (o + (i + 8) * 8 + b));
-            }
-            if constexpr (NORM) {
-                v0 *= inv[b];
-                v1 *= inv[b];
             }
             epi.store(t0 + j, i, b, v0, v1, keys);
         }
