@@ -39,7 +39,10 @@ constexpr int kBgKeysOff = 640;
 constexpr int kBgFlagOff = 704;
 constexpr int kBgPBytes = 2 * kBgWaves * 16 * 8 * 4;  // double-buffered per-wave tile partials
 constexpr int kBgLdsMax = 160 * 1024;
-constexpr int kBgU = 4;                // 16-byte weight loads per lane per step (two steps in flight)
+// 16-byte weight loads per lane per step (two steps in flight): 4, or 2 for one-tile plans (a finer
+// pipeline over a workgroup's single tile; C4 wo 11.3 -> 10.7 us, TP-8 down 9.3 -> 7.4 us; the multi-tile
+// plans lose with 2: down 31.6 -> 33.7 us) — bg_step_width
+constexpr int bg_step_width(int tpw) { return tpw == 1 ? 2 : 4; }
 
 struct BgIn {
     const float* x;       // [B][K] fp32 activations
@@ -142,7 +145,7 @@ __device__ __forceinline__ void bg_split8(const float* y, u32x4& hi, u32x4& lo) 
 //   store(t, i, b, v0, v1, kl)  final sums of tile rows i (< 8) and i + 8 for sequence b; kl = the
 //                               workgroup's per-sequence argmax keys in LDS
 //   finish(kl, group, B)        once per workgroup that ran stores, after all of them
-template <class Epi, bool NORM>
+template <class Epi, bool NORM, int kBgU = 4>
 __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restrict__ W, BgIn in, Epi epi_in) {
     Epi epi = epi_in;
     extern __shared__ __attribute__((aligned(16))) char bg_smem[];
@@ -489,8 +492,13 @@ struct BgEpiLogits {
 // Allow the kernel its full dynamic LDS (once per instantiation; call outside stream capture).
 template <class Epi, bool NORM>
 hipError_t bg_allow_lds() {
-    static const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&bgemm_kernel<Epi, NORM>),
-                                                    hipFuncAttributeMaxDynamicSharedMemorySize, kBgLdsMax);
+    static const hipError_t e = [] {
+        const hipError_t e4 = hipFuncSetAttribute(reinterpret_cast<const void*>(&bgemm_kernel<Epi, NORM, 4>),
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, kBgLdsMax);
+        const hipError_t e2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&bgemm_kernel<Epi, NORM, 2>),
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, kBgLdsMax);
+        return e4 != hipSuccess ? e4 : e2;
+    }();
     return e;
 }
 
@@ -502,10 +510,15 @@ hipError_t launch_bgemm(const __half* W, const BgIn& in_, const Epi& epi, const 
     in.splits = p.splits;
     const dim3 grid(p.groups * p.splits);
     if (in.norm_w && p.splits != 1) return hipErrorInvalidValue;  // the fused RMS runs on one split only
-    if (in.norm_w)
-        hipLaunchKernelGGL((bgemm_kernel<Epi, true>), grid, dim3(kBgThreads), p.lds, s, W, in, epi);
+    const bool u2 = bg_step_width(p.tpw) == 2;
+    if (in.norm_w && u2)
+        hipLaunchKernelGGL((bgemm_kernel<Epi, true, 2>), grid, dim3(kBgThreads), p.lds, s, W, in, epi);
+    else if (in.norm_w)
+        hipLaunchKernelGGL((bgemm_kernel<Epi, true, 4>), grid, dim3(kBgThreads), p.lds, s, W, in, epi);
+    else if (u2)
+        hipLaunchKernelGGL((bgemm_kernel<Epi, false, 2>), grid, dim3(kBgThreads), p.lds, s, W, in, epi);
     else
-        hipLaunchKernelGGL((bgemm_kernel<Epi, false>), grid, dim3(kBgThreads), p.lds, s, W, in, epi);
+        hipLaunchKernelGGL((bgemm_kernel<Epi, false, 4>), grid, dim3(kBgThreads), p.lds, s, W, in, epi);
     return hipGetLastError();
 }
 
