@@ -74,7 +74,7 @@ def parse():
     ap.add_argument("--greedy-steps", type=int, default=64, help="the greedy sanity run's length (profiling passes: 2)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample budget")
     ap.add_argument("--gemv-iters", type=int, default=20)
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r2_gemv_traffic.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r2b_gemv_traffic.json"))
     return ap.parse_args()
 
 
@@ -117,8 +117,14 @@ def cpu_baseline(budget_s: float, preset_name: str = "llama2-7b", ctx: int = CTX
                        f"projected {step:.2f} s = embed + {n_layers} x layer + head")}
 
 
+def progress(msg):
+    """A progress line on stderr (long profiled runs stay visibly alive; stdout keeps the one JSON line)."""
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     a = parse()
+    progress("start (the first torch import on a fresh box can take a minute or two)")
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -186,6 +192,7 @@ def main():
             else:
                 model.set_allreduce("rccl")
                 allreduce = "rccl (one-shot validation failed)"
+    progress("model ready, timing the step")
     for _ in range(a.warmup):
         model.step()
     barrier()
@@ -203,6 +210,7 @@ def main():
     if st["error"]:
         raise SystemExit(f"device error flag {st['error']}")
     wbytes, kvbytes = model.step_bytes()
+    progress("timed; per-family probes")
     fam = model.time_families(a.gemv_iters)
     sfl = model.time_stream(a.gemv_iters)  # the measured streaming-read floor of the same launches
     g = model.time_gemv(a.gemv_iters)
@@ -220,6 +228,7 @@ def main():
 
     # a true greedy decode beside the idempotent-step timing: 64 tokens at positions ctx-64 .. ctx-1, the
     # state (position, next token = greedy argmax) advancing on the device every step
+    progress("greedy run")
     g_steps = min(a.greedy_steps, a.ctx - 1)
     for b in range(B):
         model.set_state_seq(b, 1234 + 17 * b, a.ctx - 1 - g_steps, advance=True)
@@ -307,6 +316,7 @@ def main():
                                    "achieved_tflops": round(tflops, 2), "peak_tflops": 2500.0,
                                    "frac": round(tflops / 2500.0, 5)}
     if a.prefill_tokens > 1 and B == 1 and a.prefill_tokens <= a.ctx:
+        progress("prefill")
         # prompt prefill: positions 0..n-2 eight at a time through the MFMA projections
         n = a.prefill_tokens
         ids = [(1 + 7919 * i) % cfg.vocab_size for i in range(n)]

@@ -18,4 +18,7 @@ for c in c1 c3 c4; do
   python3 tools/step_trace.py $(find gpurun_out/prof -name "${tag}_${c}_kernel_trace.csv" | head -1) > gpurun_out/prof/${tag}_${c}_step_trace.txt
   tail -1 gpurun_out/prof/${tag}_${c}_step_trace.txt
 done
+# keep the summaries (kernel stats, step traces) within gpurun's 64 MiB copy-back: drop the raw traces
+find gpurun_out/prof -name '*_kernel_trace.csv' -delete
+find gpurun_out/prof -name '*agent_info*' -delete
 echo final done

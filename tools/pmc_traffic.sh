@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 tag=${1:-r02}; shift
 mkdir -p gpurun_out/pmc
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -s KILL 420 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc -o fetch --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --gemv-iters 1 --greedy-steps 2 "$@" > gpurun_out/pmc/bench.log 2>&1 || { echo PMC FAILED; tail -20 gpurun_out/pmc/bench.log; exit 1; }
+timeout -s KILL 420 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc -o fetch --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --gemv-iters 1 --greedy-steps 2 --prefill-tokens 0 "$@" > gpurun_out/pmc/bench.log 2>&1 || { echo PMC FAILED; tail -20 gpurun_out/pmc/bench.log; exit 1; }
 csvf=$(find gpurun_out/pmc -name 'fetch_counter_collection.csv' | head -1)  # rocprofv3 may or may not add a subdirectory
 [ -n "$csvf" ] || { echo "PMC: no counter csv"; exit 1; }
 alg=$(grep '^{' gpurun_out/pmc/bench.log | tail -1 | python3 -c "import json,sys; print(json.loads(sys.stdin.read())['roofline']['algorithmic_bytes_per_launch'])")
