@@ -498,10 +498,39 @@ __global__ void group_finalize_kernel(GroupKeyArgs a) {
 // vector holds twice the columns: the same columns per chunk, two chunks per 4096-column row instead of
 // one, so a wave's second buffer streams while the first is consumed (measured C3: 414 -> 447 tok/s;
 // a quarter U: 431).
-template <typename WT, int R, int U, bool NT, class Epi>
-static hipError_t launch_gemv_u(const WT* W, const GemvIn& in, const Epi& epi, int units, hipStream_t s) {
+//
+// Small matrices (tensor-parallel shards: TP-8 q/k/v has 768 two-row units for 4096 waves) split each
+// unit's rows over CS column parts (gemv.h gemv_block): CS = the power of two that gives every wave of the
+// chip an item, at the widest U whose chunks still cover CS parts per row (U, then 2, then 1). Full-size
+// matrices (every TP-1 projection) keep CS = 1.
+struct GemvSplit {
+    int cs, u;  // column parts per unit, vectors per lane per chunk
+};
+template <typename WT, int U>
+static GemvSplit gemv_split(int units, int cols) {
     constexpr int UW = std::is_same<WT, int8_t>::value && U >= 2 ? U / 2 : U;
-    return launch_gemv<WT, R, UW, NT>(W, in, epi, units, s);
+    const int waves = gemv_max_blocks() * (kGemvThreads / 64);
+    int need = 1;
+    while (need < 8 && units * need < waves) need *= 2;
+    const int nvec = cols / Vec16<WT>::N;
+    auto cpr = [&](int u) { return (nvec + 64 * u - 1) / (64 * u); };
+    if (need == 1) return {1, UW};
+    if (need <= cpr(UW)) return {need, UW};
+    if (UW > 2 && need <= cpr(2)) return {need, 2};
+    return {std::max(1, std::min(need, cpr(1))), 1};
+}
+template <typename WT, int R, int U, bool NT, class Epi>
+static hipError_t launch_gemv_u(const WT* W, const GemvIn& in_, const Epi& epi, int units, hipStream_t s) {
+    constexpr int UW = std::is_same<WT, int8_t>::value && U >= 2 ? U / 2 : U;
+    GemvIn in = in_;
+    const GemvSplit sp = gemv_split<WT, U>(units, in.cols);
+    in.csplit = sp.cs;
+    if (sp.cs == 1) return launch_gemv<WT, R, UW, NT>(W, in, epi, units, s);
+    if (sp.u == UW) return launch_gemv<WT, R, UW, NT, Epi, 2, true>(W, in, epi, units, s);
+    if constexpr (UW > 2) {
+        if (sp.u == 2) return launch_gemv<WT, R, 2, NT, Epi, 2, true>(W, in, epi, units, s);
+    }
+    return launch_gemv<WT, R, 1, NT, Epi, 2, true>(W, in, epi, units, s);
 }
 
 // batched decode: the attention's split merge as its own launch (attention.h attn_merge_kernel, mode 2);
@@ -560,7 +589,11 @@ struct StepRecorder {
             SLI_HIP((launch_gemv_u<WT, 1, 6, NT>((const WT*)w.down, in, e, m->D, m->stream)));
         return SLI_OK;
     }
-    static int lm_head_blocks(sli_model* m) { return gemv_blocks((m->v_n + 1) / 2); }
+    // the LM head launch's grid (its workgroups each write one argmax key): gemv_lm's split and blocks
+    static int lm_head_blocks(sli_model* m) {
+        const int units = (m->v_n + 1) / 2;
+        return gemv_blocks(units, gemv_split<WT, 4>(units, m->D).cs);
+    }
     static int gemv_lm(sli_model* m) {
         GemvIn in{m->x, m->norms + (size_t)(2 * m->L) * m->D, m->c.eps, m->D};
         EpiLogits<2> e{m->logits, m->keys, m->emb_s ? m->emb_s + m->v_lo : nullptr, m->v_n, m->v_lo, 0ull};

@@ -21,6 +21,7 @@ struct GemvIn {
     float eps;
     int cols;
     unsigned long long* stamps = nullptr;  // diagnostic (tools/gemv_lab): per-wave s_memrealtime x4
+    int csplit = 1;  // column parts per unit (gemv_block): a unit's rows split over up to csplit waves
 };
 
 constexpr int kGemvThreads = 1024;  // one persistent 16-wave workgroup per CU: x staged once per CU
@@ -235,9 +236,9 @@ __device__ __forceinline__ int gemv_unit_begin(int gwave, int nunits, int total_
     return (int)(((unsigned)gwave * (unsigned)nunits) / (unsigned)total_waves);
 }
 
-// Result slots in LDS behind the staged x: R floats per unit of the workgroup.
-inline size_t gemv_res_floats(int units, int grid, int R) {
-    return (size_t)R * ((size_t)units / grid + 2);
+// Result slots in LDS behind the staged x: R floats per (unit, column part) of the workgroup.
+inline size_t gemv_res_floats(int units, int grid, int R, int csplit = 1) {
+    return (size_t)R * csplit * ((size_t)units / grid + 2);
 }
 
 // Wave-level schedule. Wave gw of the grid owns units [gw*N/W, (gw+1)*N/W) (balanced: sizes differ by at
@@ -254,7 +255,7 @@ inline size_t gemv_res_floats(int units, int grid, int R) {
 // for the first weight chunk (staged 4-6 us into a 10-30 us launch). The epilogue (residual reads,
 // RoPE, K/V writes, logits) runs once per workgroup after the loop, one thread per unit.
 // Prologue order: input loads, first weight chunk, input commit + barrier (see XStage).
-template <typename WT, int R, int U, bool NT, class Epi, class Stage, int NB = 2>
+template <typename WT, int R, int U, bool NT, class Epi, class Stage, int NB = 2, bool SPLIT = false>
 __device__ __forceinline__ void gemv_block(const WT* __restrict__ W, const GemvIn& in, Epi& epi, Stage& stage,
                                            float* smem) {
     const float* xs = smem + kGemvLdsHead;
@@ -268,13 +269,18 @@ __device__ __forceinline__ void gemv_block(const WT* __restrict__ W, const GemvI
     const size_t row_bytes = (size_t)in.cols * sizeof(WT);
     const int nunits = epi.units();
     const int total_waves = gridDim.x * nwaves;
-    const int gw = blockIdx.x * nwaves + wave;
-    const int u_begin = gemv_unit_begin(gw, nunits, total_waves);
-    const int u_end = gemv_unit_begin(gw + 1, nunits, total_waves);
     const int ub = gemv_unit_begin(blockIdx.x * nwaves, nunits, total_waves);  // workgroup's first unit
     const int ue = gemv_unit_begin((blockIdx.x + 1) * nwaves, nunits, total_waves);
     const int cpr = (nvec + CV - 1) / CV;  // chunks per row
-    const int nsteps = (u_end - u_begin) * cpr;
+    // Column split (small matrices, e.g. tensor-parallel shards): a unit's rows are cut into CS parts of
+    // cpp chunks; the workgroup's (unit, part) items are balanced over its waves and the parts' row sums
+    // are added in part order in the epilogue. CS = 1: one item per unit, the whole row per wave.
+    const int CS = SPLIT ? in.csplit : 1;  // compile-time 1 unless the launch split the columns
+    const int cpp = (cpr + CS - 1) / CS;  // chunks per part (a part past the row end is all masked)
+    const int ni = (ue - ub) * CS;       // the workgroup's items
+    const int ib = (int)(((unsigned)wave * (unsigned)ni) / (unsigned)nwaves);
+    const int ie = (int)(((unsigned)(wave + 1) * (unsigned)ni) / (unsigned)nwaves);
+    const int nsteps = (ie - ib) * cpp;
     float* res = smem + kGemvLdsHead + in.cols;
 
     const unsigned long long t_entry = in.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -286,12 +292,18 @@ __device__ __forceinline__ void gemv_block(const WT* __restrict__ W, const GemvI
     epi.prefetch_a(pre_unit);
     __builtin_amdgcn_sched_barrier(0);  // keep every input load ahead of the weight loads
 
-    // (u, c) = unit and chunk of a step; the load position saturates at the wave's last step
-    const int u_last = max(min(u_end, nunits) - 1, 0);
-    auto load_step = [&](int u, int c, u32x4 (&w)[U][R]) {
+    // A step is (item, chunk of its part); the position (u, p, cc) advances incrementally. The load
+    // position saturates at the wave's last step (a wave without items loads a valid row it never uses).
+    struct Pos {
+        int it, u, p, cc;
+    };
+    const int it_last = max(ie - 1, ib);
+    const Pos last{it_last, min(ub + it_last / CS, nunits - 1), it_last - (it_last / CS) * CS, cpp - 1};
+    auto load_step = [&](const Pos& q, u32x4 (&w)[U][R]) {
+        const Pos& a = q.it > it_last ? last : q;
         int rows[R];
-        epi.rows(min(u, u_last), rows);
-        const int v = (u > u_last ? cpr - 1 : c) * CV + lane;
+        epi.rows(min(a.u, nunits - 1), rows);
+        const int v = (a.p * cpp + a.cc) * CV + lane;
 #pragma unroll
         for (int j = 0; j < U; ++j) {
             const int vj = min(v + j * 64, nvec - 1);  // clamp, never branch around a load
@@ -300,26 +312,31 @@ __device__ __forceinline__ void gemv_block(const WT* __restrict__ W, const GemvI
                 w[j][r] = load16<NT>(reinterpret_cast<const char*>(W) + (size_t)rows[r] * row_bytes + (size_t)vj * 16);
         }
     };
-    auto next = [&](int& u, int& c) {
-        if (++c == cpr) {
-            c = 0;
-            ++u;
+    auto next = [&](Pos& q) {
+        if (++q.cc == cpp) {
+            q.cc = 0;
+            ++q.it;
+            if (++q.p == CS) {
+                q.p = 0;
+                ++q.u;
+            }
         }
     };
     float acc[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = 0.0f;
-    auto consume_step = [&](int u, int c, const u32x4(&w)[U][R]) {
+    auto consume_step = [&](const Pos& q, const u32x4(&w)[U][R]) {
+        const int c = q.p * cpp + q.cc;
         const int v = c * CV + lane;
         if ((c + 1) * CV <= nvec)
             gemv_chunk<WT, R, U>(w, xs, v, acc);
         else
             gemv_chunk<WT, R, U, true>(w, xs, v, acc, nvec);
-        if (c == cpr - 1) {  // unit complete: its R row sums go to LDS
+        if (q.cc == cpp - 1) {  // item complete: its R partial row sums go to LDS
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const float t = wave_sum(acc[r]);
-                if (lane == 0) res[(u - ub) * R + r] = t;
+                if (lane == 0) res[((q.u - ub) * CS + q.p) * R + r] = t;
                 acc[r] = 0.0f;
             }
         }
@@ -331,12 +348,13 @@ __device__ __forceinline__ void gemv_block(const WT* __restrict__ W, const GemvI
     // no clamped load is ever issued after its data was consumed (a fresh HBM round trip at the end of
     // every wave).
     u32x4 wbuf[NB][U][R];
-    int lu = u_begin, lc = 0;  // next step to load
-    int cu = u_begin, cc = 0;  // next step to consume
+    const Pos first{ib, ub + ib / CS, ib - (ib / CS) * CS, 0};
+    Pos lq = first;  // next step to load
+    Pos cq = first;  // next step to consume
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-        load_step(lu, lc, wbuf[b]);
-        next(lu, lc);
+        load_step(lq, wbuf[b]);
+        next(lq);
     }
     __builtin_amdgcn_sched_barrier(0);
     stage.commit(smem, in);
@@ -347,24 +365,31 @@ __device__ __forceinline__ void gemv_block(const WT* __restrict__ W, const GemvI
     for (; k + NB < nsteps; k += NB) {
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
-            consume_step(cu, cc, wbuf[b]);
-            next(cu, cc);
-            load_step(lu, lc, wbuf[b]);  // step k + b + NB, or a duplicate of the wave's last step
-            next(lu, lc);
+            consume_step(cq, wbuf[b]);
+            next(cq);
+            load_step(lq, wbuf[b]);  // step k + b + NB, or a duplicate of the wave's last step
+            next(lq);
         }
     }
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
         if (k + b < nsteps) {
-            consume_step(cu, cc, wbuf[b]);
-            next(cu, cc);
+            consume_step(cq, wbuf[b]);
+            next(cq);
         }
     }
     __syncthreads();
     for (int u = ub + (int)threadIdx.x; u < ue; u += kGemvThreads) {
         int rows[R];
         epi.rows(u, rows);
-        epi.store(u, rows, res + (u - ub) * R);
+        const float* ru = res + (size_t)(u - ub) * CS * R;
+        float v[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            v[r] = ru[r];
+            for (int p = 1; p < CS; ++p) v[r] += ru[p * R + r];  // part order: deterministic
+        }
+        epi.store(u, rows, v);
     }
     epi.finish(smem);
     if (in.stamps && lane == 0) {
@@ -378,12 +403,12 @@ __device__ __forceinline__ void gemv_block(const WT* __restrict__ W, const GemvI
     }
 }
 
-template <typename WT, int R, int U, bool NT, class Epi, int NB = 2>
+template <typename WT, int R, int U, bool NT, class Epi, int NB = 2, bool SPLIT = false>
 __global__ void __launch_bounds__(kGemvThreads) gemv_kernel(const WT* __restrict__ W, GemvIn in, Epi epi_in) {
     Epi epi = epi_in;  // mutable per-thread copy (EpiLogits keeps a running key)
     extern __shared__ __attribute__((aligned(16))) float smem[];
     XStage<Vec16<WT>::N / 4> stage;
-    gemv_block<WT, R, U, NT, Epi, XStage<Vec16<WT>::N / 4>, NB>(W, in, epi, stage, smem);
+    gemv_block<WT, R, U, NT, Epi, XStage<Vec16<WT>::N / 4>, NB, SPLIT>(W, in, epi, stage, smem);
 }
 
 // the wo GEMV with its input merged from the attention's split partials (XStageMerge)
@@ -633,28 +658,33 @@ constexpr int kGemvMaxCols = 16384 - kGemvLdsHead;  // x staged in 64 KiB of LDS
 // persistent grid: one workgroup per CU of the current device (MI355X: 8 XCDs x 32 CUs = 256)
 inline int gemv_max_blocks() { return device_cus(); }
 
-// Grid: enough workgroups for every unit to have a wave, capped at the persistent size; the balanced
-// schedule in gemv_kernel spreads the units over whatever grid this returns.
-inline int gemv_blocks(int units) {
+// Grid: enough workgroups for every (unit, column part) item to have a wave, capped at the persistent
+// size; the balanced schedule in gemv_block spreads the items over whatever grid this returns.
+inline int gemv_blocks(int units, int csplit = 1) {
     const int maxb = gemv_max_blocks();
-    int b = (units + (kGemvThreads / 64) - 1) / (kGemvThreads / 64);
+    const int items = units * csplit;
+    int b = (items + (kGemvThreads / 64) - 1) / (kGemvThreads / 64);
+    b = b < units ? b : units;  // every workgroup owns at least one unit
     return b < maxb ? (b > 0 ? b : 1) : maxb;
 }
 
 template <typename WT, int R, int U, bool NT, class Epi>
 hipError_t launch_gemv_merge(const WT* W, const GemvIn& in, const Epi& epi, const AttnMergeIn& am, int units,
                              hipStream_t s) {
+    if (in.csplit != 1) return hipErrorInvalidValue;  // the merge-staged wo GEMV runs unsplit
     const int grid = gemv_blocks(units);
     const size_t lds = gemv_lds_bytes(in.cols) + sizeof(float) * gemv_res_floats(units, grid, R);
     hipLaunchKernelGGL((gemv_merge_kernel<WT, R, U, NT, Epi>), dim3(grid), dim3(kGemvThreads), lds, s, W, in, epi, am);
     return hipGetLastError();
 }
 
-template <typename WT, int R, int U, bool NT, class Epi, int NB = 2>
+template <typename WT, int R, int U, bool NT, class Epi, int NB = 2, bool SPLIT = false>
 hipError_t launch_gemv(const WT* W, const GemvIn& in, const Epi& epi, int units, hipStream_t s) {
-    const int grid = gemv_blocks(units);
-    const size_t lds = gemv_lds_bytes(in.cols) + sizeof(float) * gemv_res_floats(units, grid, R);
-    hipLaunchKernelGGL((gemv_kernel<WT, R, U, NT, Epi, NB>), dim3(grid), dim3(kGemvThreads), lds, s, W, in, epi);
+    if (!SPLIT && in.csplit != 1) return hipErrorInvalidValue;  // a split needs the SPLIT instantiation
+    const int grid = gemv_blocks(units, in.csplit);
+    const size_t lds = gemv_lds_bytes(in.cols) + sizeof(float) * gemv_res_floats(units, grid, R, in.csplit);
+    hipLaunchKernelGGL((gemv_kernel<WT, R, U, NT, Epi, NB, SPLIT>), dim3(grid), dim3(kGemvThreads), lds, s, W, in,
+                       epi);
     return hipGetLastError();
 }
 
