@@ -325,12 +325,19 @@ __global__ void __launch_bounds__(64 * WAVES) attn_partial_kernel(AttnArgs<KT> a
 // consumer is the MFMA projection, whose every workgroup stages the whole activation, so merging in its
 // staging would re-read the partials once per workgroup). Freed of the merge, the attention workgroups
 // end right after their partial store: at C4 the 1024 workgroups run in two residency rounds, and the
-// first round's slots free sooner. grid: n_kv_heads workgroups of kAttnMergeThreads.
+// first round's slots free sooner. grid: n_kv_heads * attn_merge_wgs(G * HD) workgroups of
+// kAttnMergeThreads: every thread merges ONE output (q head g, dim d), so the launch is one round trip to
+// the partials (C4: two passes of 256 threads per kv head took 5.9 us).
 constexpr int kAttnMergeThreads = 256;
+__host__ __device__ constexpr int attn_merge_wgs(int outputs) {
+    return (outputs + kAttnMergeThreads - 1) / kAttnMergeThreads;
+}
 template <typename KT, int HD, int G>
 __global__ void __launch_bounds__(kAttnMergeThreads) attn_merge_kernel(AttnArgs<KT> a) {
-    const int kvh = blockIdx.x;
-    attn_merge<HD, G>(a.part, a.out, kvh, a.max_splits, attn_live_splits<KT, HD, G>(a, kvh), 0, kAttnMergeThreads);
+    constexpr int MS = attn_merge_wgs(G * HD);
+    const int kvh = blockIdx.x / MS, j = blockIdx.x - kvh * MS;
+    attn_merge<HD, G>(a.part, a.out, kvh, a.max_splits, attn_live_splits<KT, HD, G>(a, kvh), -j * kAttnMergeThreads,
+                      MS * kAttnMergeThreads);
 }
 
 }  // namespace sli

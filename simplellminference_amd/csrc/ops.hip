@@ -187,10 +187,10 @@ static int mha_launch_hd(const float* q, const KT* kc, const KT* vc, float* out,
     if (defer_merge == 2) {
         const dim3 mb(kAttnMergeThreads);
         switch (g) {
-            case 1: hipLaunchKernelGGL((attn_merge_kernel<KT, HD, 1>), dim3(Hkv), mb, 0, s, a); break;
-            case 2: hipLaunchKernelGGL((attn_merge_kernel<KT, HD, 2>), dim3(Hkv), mb, 0, s, a); break;
-            case 4: hipLaunchKernelGGL((attn_merge_kernel<KT, HD, 4>), dim3(Hkv), mb, 0, s, a); break;
-            default: hipLaunchKernelGGL((attn_merge_kernel<KT, HD, 8>), dim3(Hkv), mb, 0, s, a); break;
+            case 1: hipLaunchKernelGGL((attn_merge_kernel<KT, HD, 1>), dim3(Hkv * attn_merge_wgs(HD)), mb, 0, s, a); break;
+            case 2: hipLaunchKernelGGL((attn_merge_kernel<KT, HD, 2>), dim3(Hkv * attn_merge_wgs(2 * HD)), mb, 0, s, a); break;
+            case 4: hipLaunchKernelGGL((attn_merge_kernel<KT, HD, 4>), dim3(Hkv * attn_merge_wgs(4 * HD)), mb, 0, s, a); break;
+            default: hipLaunchKernelGGL((attn_merge_kernel<KT, HD, 8>), dim3(Hkv * attn_merge_wgs(8 * HD)), mb, 0, s, a); break;
         }
         SLI_HIP(hipGetLastError());
     }
