@@ -117,6 +117,24 @@ def cpu_baseline(budget_s: float, preset_name: str = "llama2-7b", ctx: int = CTX
                        f"projected {step:.2f} s = embed + {n_layers} x layer + head")}
 
 
+def _oneshot_opened(model, dist, torch, mode) -> bool:
+    """Map every rank's one-shot all-reduce buffer (IPC over the gloo group); True only if it worked on
+    EVERY rank (a rank that failed still joins the collective vote, so no rank waits on a peer that is not
+    there). Forced --tp-allreduce oneshot re-raises the failure."""
+    from simplellminference_amd import tp
+    err = None
+    try:
+        tp.open_oneshot(model)
+    except Exception as e:  # noqa: BLE001 - reported, voted on, then RCCL carries the step
+        err = e
+        progress(f"one-shot buffers unavailable on this rank: {e}")
+    flag = torch.tensor([0 if err else 1], dtype=torch.int32)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if err is not None and mode == "oneshot":
+        raise err
+    return flag.item() == 1
+
+
 def progress(msg):
     """A progress line on stderr (long profiled runs stay visibly alive; stdout keeps the one JSON line)."""
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
@@ -173,10 +191,10 @@ def main():
             tp.open_oneshot(model)
             model.set_allreduce("oneshot")
             allreduce = "oneshot (SLI_DEBUG_NOCOMM: not validated against rccl)"
+        elif a.tp_allreduce != "rccl" and not _oneshot_opened(model, dist, torch, a.tp_allreduce):
+            allreduce = "rccl (one-shot buffers could not be mapped on every rank)"
         elif a.tp_allreduce != "rccl":
-            from simplellminference_amd import tp
             import numpy as np
-            tp.open_oneshot(model)
             model.step()  # RCCL reference step (idempotent: position ctx-1 is recomputed)
             ref = model.logits()[0].copy()
             model.set_allreduce("oneshot")
@@ -191,6 +209,8 @@ def main():
                 raise SystemExit("one-shot all-reduce disagrees with RCCL")
             else:
                 model.set_allreduce("rccl")
+                for b in range(B):  # clears a timed-out one-shot's device error flag
+                    model.set_state_seq(b, 1234 + 17 * b, a.ctx - 1, advance=False)
                 allreduce = "rccl (one-shot validation failed)"
     progress("model ready, timing the step")
     for _ in range(a.warmup):

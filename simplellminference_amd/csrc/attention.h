@@ -53,7 +53,10 @@ __device__ __forceinline__ int attn_pos(const AttnArgs<KT>& a, int kvh) {
 // same for every WAVES; WAVES trades registers for latency hiding: 16 waves of 4 (MHA, GQA-2: each
 // wave starts computing as soon as its own few rows land, 4 waves per SIMD overlap), 8 waves of 8
 // (GQA-4) or 4 waves of 16 (GQA-8, whose G query heads need the register room of one wave per SIMD).
-constexpr int kAttnSlots = 64;
+#ifndef SLI_ATTN_SLOTS
+#define SLI_ATTN_SLOTS 64
+#endif
+constexpr int kAttnSlots = SLI_ATTN_SLOTS;
 constexpr int kAttnMaxWgSplits = 128;  // combine-kernel capacity
 
 template <typename KT, int HD>
