@@ -494,44 +494,8 @@ __global__ void group_finalize_kernel(GroupKeyArgs a) {
 }
 
 // ---------------------------------------------------------------- the step
-// Vectors in flight per lane: the per-shape U (fp16, tools/gemv_lab) halved for int8, whose 16-byte
-// vector holds twice the columns: the same columns per chunk, two chunks per 4096-column row instead of
-// one, so a wave's second buffer streams while the first is consumed (measured C3: 414 -> 447 tok/s;
-// a quarter U: 431).
-//
-// Small matrices (tensor-parallel shards: TP-8 q/k/v has 768 two-row units for 4096 waves) split each
-// unit's rows over CS column parts (gemv.h gemv_block): CS = the power of two that gives every wave of the
-// chip an item, at the widest U whose chunks still cover CS parts per row (U, then 2, then 1). Full-size
-// matrices (every TP-1 projection) keep CS = 1.
-struct GemvSplit {
-    int cs, u;  // column parts per unit, vectors per lane per chunk
-};
-template <typename WT, int U>
-static GemvSplit gemv_split(int units, int cols) {
-    constexpr int UW = std::is_same<WT, int8_t>::value && U >= 2 ? U / 2 : U;
-    const int waves = gemv_max_blocks() * (kGemvThreads / 64);
-    int need = 1;
-    while (need < 8 && units * need < waves) need *= 2;
-    const int nvec = cols / Vec16<WT>::N;
-    auto cpr = [&](int u) { return (nvec + 64 * u - 1) / (64 * u); };
-    if (need == 1) return {1, UW};
-    if (need <= cpr(UW)) return {need, UW};
-    if (UW > 2 && need <= cpr(2)) return {need, 2};
-    return {std::max(1, std::min(need, cpr(1))), 1};
-}
-template <typename WT, int R, int U, bool NT, class Epi>
-static hipError_t launch_gemv_u(const WT* W, const GemvIn& in_, const Epi& epi, int units, hipStream_t s) {
-    constexpr int UW = std::is_same<WT, int8_t>::value && U >= 2 ? U / 2 : U;
-    GemvIn in = in_;
-    const GemvSplit sp = gemv_split<WT, U>(units, in.cols);
-    in.csplit = sp.cs;
-    if (sp.cs == 1) return launch_gemv<WT, R, UW, NT>(W, in, epi, units, s);
-    if (sp.u == UW) return launch_gemv<WT, R, UW, NT, Epi, 2, true>(W, in, epi, units, s);
-    if constexpr (UW > 2) {
-        if (sp.u == 2) return launch_gemv<WT, R, 2, NT, Epi, 2, true>(W, in, epi, units, s);
-    }
-    return launch_gemv<WT, R, 1, NT, Epi, 2, true>(W, in, epi, units, s);
-}
+// launch_gemv_u / gemv_split: gemv.h (shared with the op-level sli_matmul)
+
 
 // batched decode: the attention's split merge as its own launch (attention.h attn_merge_kernel, mode 2);
 // SLI_ATTN_MERGE_LAUNCH=0 keeps the last-arriver merge inside the attention launch (A/B measurement)

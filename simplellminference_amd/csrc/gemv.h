@@ -11,6 +11,9 @@
 //     (plain store, residual add, RoPE + KV-cache write, SwiGLU, logits + argmax keys).
 // Grid-stride over units so a launch is sized to the chip, not to the matrix.
 #pragma once
+#include <algorithm>
+#include <type_traits>
+
 #include "common.h"
 
 namespace sli {
@@ -686,6 +689,45 @@ hipError_t launch_gemv(const WT* W, const GemvIn& in, const Epi& epi, int units,
     hipLaunchKernelGGL((gemv_kernel<WT, R, U, NT, Epi, NB, SPLIT>), dim3(grid), dim3(kGemvThreads), lds, s, W, in,
                        epi);
     return hipGetLastError();
+}
+
+// Vectors in flight per lane: the per-shape U (fp16, tools/gemv_lab) halved for int8, whose 16-byte
+// vector holds twice the columns: the same columns per chunk, two chunks per 4096-column row instead of
+// one, so a wave's second buffer streams while the first is consumed (measured C3: 414 -> 447 tok/s;
+// a quarter U: 431).
+//
+// Small matrices (tensor-parallel shards: TP-8 q/k/v has 768 two-row units for 4096 waves) split each
+// unit's rows over CS column parts (gemv.h gemv_block): CS = the power of two that gives every wave of the
+// chip an item, at the widest U whose chunks still cover CS parts per row (U, then 2, then 1). Full-size
+// matrices (every TP-1 projection) keep CS = 1.
+struct GemvSplit {
+    int cs, u;  // column parts per unit, vectors per lane per chunk
+};
+template <typename WT, int U>
+inline GemvSplit gemv_split(int units, int cols) {
+    constexpr int UW = std::is_same<WT, int8_t>::value && U >= 2 ? U / 2 : U;
+    const int waves = gemv_max_blocks() * (kGemvThreads / 64);
+    int need = 1;
+    while (need < 8 && units * need < waves) need *= 2;
+    const int nvec = cols / Vec16<WT>::N;
+    auto cpr = [&](int u) { return (nvec + 64 * u - 1) / (64 * u); };
+    if (need == 1) return {1, UW};
+    if (need <= cpr(UW)) return {need, UW};
+    if (UW > 2 && need <= cpr(2)) return {need, 2};
+    return {std::max(1, std::min(need, cpr(1))), 1};
+}
+template <typename WT, int R, int U, bool NT, class Epi>
+hipError_t launch_gemv_u(const WT* W, const GemvIn& in_, const Epi& epi, int units, hipStream_t s) {
+    constexpr int UW = std::is_same<WT, int8_t>::value && U >= 2 ? U / 2 : U;
+    GemvIn in = in_;
+    const GemvSplit sp = gemv_split<WT, U>(units, in.cols);
+    in.csplit = sp.cs;
+    if (sp.cs == 1) return launch_gemv<WT, R, UW, NT>(W, in, epi, units, s);
+    if (sp.u == UW) return launch_gemv<WT, R, UW, NT, Epi, 2, true>(W, in, epi, units, s);
+    if constexpr (UW > 2) {
+        if (sp.u == 2) return launch_gemv<WT, R, 2, NT, Epi, 2, true>(W, in, epi, units, s);
+    }
+    return launch_gemv<WT, R, 1, NT, Epi, 2, true>(W, in, epi, units, s);
 }
 
 }  // namespace sli

@@ -145,7 +145,7 @@ static int matmul_dispatch(const float* x, const WT* w, const float* rscale, flo
     if (vec_ok) {
         EpiStore<2> epi{y, nullptr, rscale, scale, rows};
         GemvIn in{x, nullptr, 0.0f, cols};
-        SLI_HIP((launch_gemv<WT, 2, 4, true>(w, in, epi, (rows + 1) / 2, s)));
+        SLI_HIP((launch_gemv_u<WT, 2, 4, true>(w, in, epi, (rows + 1) / 2, s)));  // column split below 4096 units
     } else {
         const int blocks = std::min(gemv_max_blocks(), (rows + 3) / 4);
         hipLaunchKernelGGL(gemv_scalar_kernel<WT>, dim3(blocks), dim3(kGemvThreads), 0, s, w, x, rscale, y, rows,

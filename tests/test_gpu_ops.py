@@ -40,7 +40,10 @@ def test_matmul_f32(gpu, oracle, rows, cols):
     assert np.all(np.abs(got - want) <= bound + 1e-30), np.abs(got - want).max()
 
 
-@pytest.mark.parametrize("rows,cols", [(4096, 4096), (11008, 4096), (4096, 11008), (32000, 4096), (768, 256)])
+# (256 / 1000 / 2048 rows: fewer two-row units than the chip's 4096 waves, so gemv.h's column split cuts
+# each unit's rows over 8 / 8 / 4 waves of its workgroup — the tensor-parallel shard path)
+@pytest.mark.parametrize("rows,cols", [(4096, 4096), (11008, 4096), (4096, 11008), (32000, 4096), (768, 256),
+                                       (256, 4096), (1000, 4096), (2048, 2048), (1376, 4096)])
 def test_matmul_f16_weights(gpu, oracle, rows, cols):
     torch = gpu
     from simplellminference_amd import ops
@@ -52,7 +55,7 @@ def test_matmul_f16_weights(gpu, oracle, rows, cols):
     _close(got, want, rtol=1e-4, atol=1e-4)  # fp32 accumulation on identical fp16 weights
 
 
-@pytest.mark.parametrize("rows,cols", [(4096, 4096), (512, 11008), (100, 256)])
+@pytest.mark.parametrize("rows,cols", [(4096, 4096), (512, 11008), (100, 256), (200, 4096), (1536, 4096)])
 def test_matmul_i8_weights(gpu, oracle, rows, cols):
     torch = gpu
     from simplellminference_amd import ops
