@@ -528,7 +528,12 @@ struct StepRecorder {
         EpiStore<1> e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, w.wo_s, 1.0f, m->D};
         const AttnMergeIn am{m->part, &m->st->pos, attn_max_splits(m), attn_wg_positions(m->c.kv_dtype, m->hd), m->hd};
         constexpr int UW = 2;  // int8 too (tools/gemv_lab i8: R1U2 7.5 us vs R1U1 7.95 on the 4096x4096 shape)
-        SLI_HIP((launch_gemv_merge<WT, 1, UW, NT>((const WT*)w.wo, in, e, am, m->D, m->stream)));
+        // contexts past 8 splits (ctx > 2048 at hd 128 fp16): the 16-split input batch (ctx 4096 wo: 13.6 us
+        // with splits 8..15 read one by one during the merge)
+        if (am.max_splits > 8)
+            SLI_HIP((launch_gemv_merge<WT, 1, UW, NT, EpiStore<1>, 16>((const WT*)w.wo, in, e, am, m->D, m->stream)));
+        else
+            SLI_HIP((launch_gemv_merge<WT, 1, UW, NT>((const WT*)w.wo, in, e, am, m->D, m->stream)));
         return SLI_OK;
     }
     static int attn_max_splits(sli_model* m) {

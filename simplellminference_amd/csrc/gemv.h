@@ -415,12 +415,12 @@ __global__ void __launch_bounds__(kGemvThreads) gemv_kernel(const WT* __restrict
 }
 
 // the wo GEMV with its input merged from the attention's split partials (XStageMerge)
-template <typename WT, int R, int U, bool NT, class Epi>
+template <typename WT, int R, int U, bool NT, class Epi, int NS = 8>
 __global__ void __launch_bounds__(kGemvThreads) gemv_merge_kernel(const WT* __restrict__ W, GemvIn in, Epi epi_in,
                                                                   AttnMergeIn am) {
     Epi epi = epi_in;
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    XStageMerge<Vec16<WT>::N / 4> stage{am};
+    XStageMerge<Vec16<WT>::N / 4, NS> stage{am};
     gemv_block<WT, R, U, NT>(W, in, epi, stage, smem);
 }
 
@@ -671,13 +671,16 @@ inline int gemv_blocks(int units, int csplit = 1) {
     return b < maxb ? (b > 0 ? b : 1) : maxb;
 }
 
-template <typename WT, int R, int U, bool NT, class Epi>
+// NS: split partials a thread loads with its input (every live split of a context up to NS * ppwg
+// positions in one batch; more splits are read from memory one by one during the merge)
+template <typename WT, int R, int U, bool NT, class Epi, int NS = 8>
 hipError_t launch_gemv_merge(const WT* W, const GemvIn& in, const Epi& epi, const AttnMergeIn& am, int units,
                              hipStream_t s) {
     if (in.csplit != 1) return hipErrorInvalidValue;  // the merge-staged wo GEMV runs unsplit
     const int grid = gemv_blocks(units);
     const size_t lds = gemv_lds_bytes(in.cols) + sizeof(float) * gemv_res_floats(units, grid, R);
-    hipLaunchKernelGGL((gemv_merge_kernel<WT, R, U, NT, Epi>), dim3(grid), dim3(kGemvThreads), lds, s, W, in, epi, am);
+    hipLaunchKernelGGL((gemv_merge_kernel<WT, R, U, NT, Epi, NS>), dim3(grid), dim3(kGemvThreads), lds, s, W, in, epi,
+                       am);
     return hipGetLastError();
 }
 
