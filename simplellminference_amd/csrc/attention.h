@@ -71,6 +71,7 @@ struct AttnGeom {
 // tools/attn_lab (profiles/r03_attn_lab.txt): MHA / GQA-2 16 waves, GQA-4 8, GQA-8 4; V loaded after the
 // scores (K and V never live together) for GQA-2 and GQA-4. MHA (57 VGPRs either way) issues K and V
 // together: C1 attention 9.17 -> 8.92 us in the step (round 2, tools/ab_variants.sh).
+// A/B knobs (variant builds, tools/ab_variants.sh); the defaults are the measured best.
 #ifndef SLI_ATTN_WAVES_MHA
 #define SLI_ATTN_WAVES_MHA 16
 #endif
