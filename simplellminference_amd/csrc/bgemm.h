@@ -43,10 +43,15 @@ constexpr int kBgLdsMax = 160 * 1024;
 // pipeline over a workgroup's single tile; C4 wo 11.3 -> 10.7 us, TP-8 down 9.3 -> 7.4 us; the multi-tile
 // plans lose with 2: down 31.6 -> 33.7 us) — bg_step_width
 constexpr int bg_step_width(int tpw) { return tpw == 1 ? 2 : 4; }
-// A plan whose waves own 7 k-blocks of every tile (C4 down: K 14336 over 4 splits) streams each tile as ONE
-// 7-vector step instead of 4 + 3 (the second step's fourth load a clamped duplicate): down 31.6 -> 29.4 us.
+// A plan whose waves own 6 or 7 k-blocks of every tile (C4 down: K 14336 over 4 splits, 7; the prefill's
+// Llama-2 down: K 11008 over 4 splits, 6) streams each tile as ONE 7-vector step instead of 4 + 3 / 4 + 2
+// (clamped duplicates in the second step): C4 down 31.6 -> 29.4 us, 512-token prefill +1.5 %.
+#ifndef SLI_BG_U7_FROM
+#define SLI_BG_U7_FROM 6
+#endif
 inline bool bg_seven_blocks(int splits, int K) {
-    return ((((K >> 5) + splits - 1) / splits) + kBgWaves - 1) / kBgWaves == 7;
+    const int bpw = ((((K >> 5) + splits - 1) / splits) + kBgWaves - 1) / kBgWaves;
+    return bpw >= SLI_BG_U7_FROM && bpw <= 7;
 }
 
 struct BgIn {
