@@ -103,6 +103,7 @@ struct sli_model {
     char* os_buf = nullptr;                  // this rank's comm buffer (uncached device memory, IPC-exported)
     char* os_peer[sli::kOsMaxRanks] = {};    // every rank's buffer mapped here (own included)
     bool os_open = false;
+    bool os_dead = false;                    // a one-shot wait timed out: set_allreduce(ONESHOT) is refused
     unsigned* os_epoch = nullptr;            // one-shot call counter
     int os_nmax = 0;
     size_t os_bytes = 0;
@@ -948,6 +949,23 @@ static int download_states(sli_model* m, std::vector<DevState>& h) {
     return SLI_OK;
 }
 
+// Device-side error bits (DevState::error: a bounded spin of the persistent step or of the one-shot
+// all-reduce gave up, leaving stale outputs) surfaced as a status: every predict path calls this after its
+// final stream sync, so a step that returned early never yields SLI_OK with garbage tokens.
+static int check_device_errors(sli_model* m) {
+    std::vector<DevState> h;
+    SLI_TRY(download_states(m, h));
+    int bits = 0;
+    for (const DevState& d : h) bits |= d.error;
+    if (bits == 0) return SLI_OK;
+    if (bits & kOsErrTimeout) m->os_dead = true;  // epochs may disagree across ranks from here on
+    std::string why;
+    if (bits & kPsErrTimeout) why += " persistent-step barrier timed out;";
+    if (bits & kEsErrTimeout) why += " stream-engine hand-off timed out;";
+    if (bits & kOsErrTimeout) why += " one-shot all-reduce timed out (the one-shot path is now refused);";
+    return fail(SLI_ERR_STATE, "device error bits 0x" + std::to_string(bits) + ":" + why + " outputs are stale");
+}
+
 static void destroy(sli_model* m) {
     if (!m) return;
     (void)hipSetDevice(m->c.device);
@@ -1386,7 +1404,7 @@ extern "C" int sli_model_predict_prefill(sli_model* m, const int32_t* prompt, in
     }
     SLI_HIP(hipMemcpyAsync(tokens_out, m->hist, sizeof(int32_t) * max_length, hipMemcpyDeviceToHost, m->stream));
     SLI_HIP(hipStreamSynchronize(m->stream));
-    return SLI_OK;
+    return check_device_errors(m);
 }
 
 extern "C" {
@@ -1488,7 +1506,7 @@ int sli_model_predict_batch(sli_model* m, const int32_t* prompts, const int32_t*
         SLI_HIP(hipMemcpyAsync(tokens_out + (size_t)b * max_length, m->hist + (size_t)b * (m->T + 1),
                                sizeof(int32_t) * max_length, hipMemcpyDeviceToHost, m->stream));
     SLI_HIP(hipStreamSynchronize(m->stream));
-    return SLI_OK;
+    return check_device_errors(m);
 }
 
 int sli_model_predict(sli_model* m, const int32_t* prompt, int32_t n_prompt, int32_t max_length, int32_t* tokens_out,
@@ -1675,6 +1693,11 @@ int sli_model_set_allreduce(sli_model* m, int32_t mode) {
     SLI_CHECK(m, SLI_ERR_ARG, "null model");
     SLI_CHECK(mode == SLI_ALLREDUCE_RCCL || mode == SLI_ALLREDUCE_ONESHOT, SLI_ERR_ARG, "unknown all-reduce mode");
     SLI_CHECK(mode == SLI_ALLREDUCE_RCCL || m->os_open, SLI_ERR_STATE, "one-shot all-reduce: open the peers first");
+    SLI_CHECK(mode == SLI_ALLREDUCE_RCCL || !m->os_dead, SLI_ERR_STATE,
+              "one-shot all-reduce: a wait timed out earlier, the ranks' epochs may disagree");
+    // the fp32 sum moves float4s and the key exchange 2*B floats: both must fit the slot exactly
+    SLI_CHECK(mode == SLI_ALLREDUCE_RCCL || ((m->B * m->D) % 4 == 0 && m->B * m->D <= m->os_nmax && 2 * m->B <= m->os_nmax),
+              SLI_ERR_SHAPE, "one-shot all-reduce: B*D must be a multiple of 4 within the comm slot");
     SLI_CHECK(mode == SLI_ALLREDUCE_RCCL || m->exec == SLI_EXEC_LAUNCHES, SLI_ERR_STATE,
               "tensor parallelism runs the launch graph");
     if (mode != m->ar_mode) {
@@ -1971,6 +1994,7 @@ int sli_tp_group_predict_batch(sli_tp_group* g, const int32_t* prompts, const in
         SLI_HIP(hipMemcpyAsync(tokens_out + (size_t)b * max_length, m0->hist + (size_t)b * (m0->T + 1),
                                sizeof(int32_t) * max_length, hipMemcpyDeviceToHost, g->stream));
     SLI_HIP(hipStreamSynchronize(g->stream));
+    for (sli_model* m : g->ranks) SLI_TRY(check_device_errors(m));
     return SLI_OK;
 }
 

@@ -82,7 +82,14 @@ __global__ void __launch_bounds__(1024) oneshot_kernel(OneShotArgs a) {
         }
     }
     __syncthreads();
-    if (abort) return;
+    if (abort) {
+        // stay in step with the peers that did not time out (they advance the epoch), and make the stale
+        // result loud: NaN instead of the previous call's values (DevState::error already records it)
+        if constexpr (OP == 0)
+            for (int i = tid; i < a.n; i += blockDim.x) a.dst[i] = __builtin_nanf("");
+        if (tid == 0) *a.epoch = e;
+        return;
+    }
     char* mine = a.peers[a.rank];
     if constexpr (OP == 0) {
         for (int i = tid; i < n4; i += blockDim.x) {

@@ -393,21 +393,6 @@ class TPGroup:
     def forward(self, token: int, pos: int) -> np.ndarray:
         return self.forward_batch([token] * self.batch, [pos] * self.batch)[0]
 
-    def prefill(self, prompt_ids):
-        """Run prompt positions 0..n-2 through the layers 8 at a time (MFMA projections) and leave the state at
-        the last prompt token, so the next step() yields the first greedy token (sli_model_prefill)."""
-        p = np.ascontiguousarray(prompt_ids, np.int32)
-        call("sli_model_prefill", self._h, p.ctypes.data_as(ctypes.c_void_p), p.size)
-
-    def predict_prefill(self, prompt_ids, max_length: int, want_logits: bool = False):
-        """predict() with the prompt prefilled; logits rows of positions < len(prompt) - 1 are NaN."""
-        p = np.ascontiguousarray(prompt_ids, np.int32)
-        toks = np.empty(max_length, np.int32)
-        logits = np.empty((max_length, self.local_vocab), np.float32) if want_logits else None
-        call("sli_model_predict_prefill", self._h, p.ctypes.data_as(ctypes.c_void_p), p.size, max_length,
-             toks.ctypes.data_as(ctypes.c_void_p), logits.ctypes.data_as(ctypes.c_void_p) if want_logits else None)
-        return (toks, logits) if want_logits else toks
-
     def predict_batch(self, prompts, max_length: int, want_logits: bool = False):
         if len(prompts) != self.batch:
             raise ValueError(f"need {self.batch} prompts")

@@ -25,7 +25,7 @@
 //   issue chunk c + D − 1 into slot (c − 1) % D
 //   compute chunk c from slot c % D
 #pragma once
-#include "attention.h"
+#include "../simplellminference_amd/csrc/attention.h"
 
 namespace sli {
 

@@ -1,4 +1,4 @@
-// attn_stream_lab.hip — diagnostic: the LDS-streamed decode attention (csrc/attn_stream.h) against the
+// attn_stream_lab.hip — diagnostic: the LDS-streamed decode attention (tools/attn_stream.h) against the
 // register-staged kernel (csrc/attention.h) on the C1 (MHA, ctx 2048) and C4 (batch 8 x GQA-4, ctx 4096)
 // shapes: merged outputs compared, then both timed over NL distinct K/V caches in a replayed hipGraph
 // (the merge launch included for both).
@@ -10,7 +10,7 @@
 #include <cstdio>
 #include <vector>
 
-#include "../simplellminference_amd/csrc/attn_stream.h"
+#include "attn_stream.h"
 
 using namespace sli;
 
