@@ -41,6 +41,8 @@ CTX = 2048
 CPU_CALIBRATION = round(0.619 / 0.439, 3)  # port / reference CPU step time on the probe shape
 FAMILY_KERNELS = {
     False: {"step": "ps_step_kernel (the whole decode step as one persistent launch: 5 phases x 32 layers + LM head)",
+            "stream_step": ("es_step_kernel (the whole decode step as one launch: a loader wave per CU streams every "
+                            "weight and K/V byte through an LDS ring, 8 consumer waves per CU)"),
             "qkv": "gemv_kernel<EpiQKV> (RMSNorm + [wq;wk;wv] GEMV + RoPE + K/V write)",
             "attention": "attn_partial_kernel (split-context flash decode + last-arriver merge)",
             "wo": "gemv_kernel<EpiStore, U=2> (wo GEMV + residual add)",
@@ -62,9 +64,10 @@ def parse():
     ap.add_argument("--preset", default="llama2-7b")
     ap.add_argument("--ctx", type=int, default=CTX)
     ap.add_argument("--batch", type=int, default=1, help="sequences decoding in lockstep (MFMA projections if > 1)")
-    ap.add_argument("--exec", default="launches", choices=["launches", "persistent"],
-                    help="launches: one graph of fused launches (default, fastest measured); persistent: the whole "
-                         "step as one launch (batch 1, TP 1; DESIGN.md §4)")
+    ap.add_argument("--exec", default="launches", choices=["launches", "persistent", "stream"],
+                    help="launches: one graph of fused launches; persistent: the whole step as one launch with grid "
+                         "barriers; stream: the whole step as one launch around an LDS-DMA weight ring (batch 1, "
+                         "TP 1; DESIGN.md §4)")
     ap.add_argument("--tp-allreduce", default="auto", choices=["auto", "rccl", "oneshot"],
                     help="TP all-reduce: auto = the one-shot xGMI kernel if a validation step against RCCL agrees on "
                          "every rank, else RCCL")
@@ -244,9 +247,9 @@ def main():
     fam = model.time_families(a.gemv_iters)
     sfl = model.time_stream(a.gemv_iters)  # the measured streaming-read floor of the same launches
     g = model.time_gemv(a.gemv_iters)
-    if exec_mode == "persistent":
-        # the step IS one kernel (ps_step_kernel): its algorithmic bytes (all weights + the live K/V) per launch
-        dom = "step"
+    if exec_mode in ("persistent", "stream"):
+        # the step IS one kernel: its algorithmic bytes (all weights + the live K/V) per launch
+        dom = "step" if exec_mode == "persistent" else "stream_step"
         d = {"avg_us": model.time_steps(a.gemv_iters), "bytes_per_launch": wbytes + kvbytes, "launches_per_step": 1}
         step_dev_us = d["avg_us"]
     else:
@@ -318,8 +321,8 @@ def main():
                      "launches_per_step": d["launches_per_step"],
                      "share_of_step_device_time": round(d["avg_us"] * d["launches_per_step"] / step_dev_us, 4),
                      "families_note": ("per-family timing of the launch path's kernels (the same arithmetic; "
-                                       "the persistent step runs them as phases of one launch)"
-                                       if exec_mode == "persistent" else "the step's launches by family"),
+                                       "the one-launch step runs them as ops of one launch)"
+                                       if exec_mode != "launches" else "the step's launches by family"),
                      "families": {f: {"avg_launch_us": round(v["avg_us"], 3),
                                       "bytes_per_launch": round(v["bytes_per_launch"]),
                                       "launches_per_step": v["launches_per_step"],
