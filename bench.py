@@ -41,8 +41,6 @@ CTX = 2048
 CPU_CALIBRATION = round(0.619 / 0.439, 3)  # port / reference CPU step time on the probe shape
 FAMILY_KERNELS = {
     False: {"step": "ps_step_kernel (the whole decode step as one persistent launch: 5 phases x 32 layers + LM head)",
-            "stream_step": ("es_step_kernel (the whole decode step as one launch: a loader wave per CU streams every "
-                            "weight and K/V byte through an LDS ring, 8 consumer waves per CU)"),
             "qkv": "gemv_kernel<EpiQKV> (RMSNorm + [wq;wk;wv] GEMV + RoPE + K/V write)",
             "attention": "attn_partial_kernel (split-context flash decode + last-arriver merge)",
             "wo": "gemv_kernel<EpiStore, U=2> (wo GEMV + residual add)",
@@ -64,10 +62,9 @@ def parse():
     ap.add_argument("--preset", default="llama2-7b")
     ap.add_argument("--ctx", type=int, default=CTX)
     ap.add_argument("--batch", type=int, default=1, help="sequences decoding in lockstep (MFMA projections if > 1)")
-    ap.add_argument("--exec", default="launches", choices=["launches", "persistent", "stream"],
-                    help="launches: one graph of fused launches; persistent: the whole step as one launch with grid "
-                         "barriers; stream: the whole step as one launch around an LDS-DMA weight ring (batch 1, "
-                         "TP 1; DESIGN.md §4)")
+    ap.add_argument("--exec", default="launches", choices=["launches", "persistent"],
+                    help="launches: one graph of fused launches (default, fastest measured); persistent: the whole "
+                         "step as one launch with grid barriers (batch 1, TP 1; DESIGN.md §4)")
     ap.add_argument("--tp-allreduce", default="auto", choices=["auto", "rccl", "oneshot"],
                     help="TP all-reduce: auto = the one-shot xGMI kernel if a validation step against RCCL agrees on "
                          "every rank, else RCCL")
@@ -247,9 +244,9 @@ def main():
     fam = model.time_families(a.gemv_iters)
     sfl = model.time_stream(a.gemv_iters)  # the measured streaming-read floor of the same launches
     g = model.time_gemv(a.gemv_iters)
-    if exec_mode in ("persistent", "stream"):
-        # the step IS one kernel: its algorithmic bytes (all weights + the live K/V) per launch
-        dom = "step" if exec_mode == "persistent" else "stream_step"
+    if exec_mode == "persistent":
+        # the step IS one kernel (ps_step_kernel): its algorithmic bytes (all weights + the live K/V) per launch
+        dom = "step"
         d = {"avg_us": model.time_steps(a.gemv_iters), "bytes_per_launch": wbytes + kvbytes, "launches_per_step": 1}
         step_dev_us = d["avg_us"]
     else:

@@ -202,12 +202,8 @@ int sli_model_get_history(sli_model* m, int32_t seq, int32_t n, int32_t* out);
  *  SLI_EXEC_LAUNCHES   one hipGraph of ~5 fused launches per layer (every configuration);
  *  SLI_EXEC_PERSISTENT the whole step as ONE persistent launch (one workgroup per CU, grid barriers between
  *                      phases, the next phase's weights streamed before each barrier): batch 1, no tensor
- *                      parallelism, 1 or 2 heads per kv head; SLI_ERR_STATE otherwise;
- *  SLI_EXEC_STREAM     the whole step as ONE persistent launch around an LDS-DMA weight ring per CU: a loader
- *                      wave streams every weight / K-V byte of the step in order and never waits for an
- *                      activation; consumer waves wait for each op's input (per-op arrival counters) and
- *                      consume the ring: batch 1, no tensor parallelism, 1, 2 or 4 heads per kv head. */
-enum { SLI_EXEC_LAUNCHES = 0, SLI_EXEC_PERSISTENT = 1, SLI_EXEC_STREAM = 2 };
+ *                      parallelism, 1 or 2 heads per kv head; SLI_ERR_STATE otherwise. */
+enum { SLI_EXEC_LAUNCHES = 0, SLI_EXEC_PERSISTENT = 1 };
 int sli_model_set_exec(sli_model* m, int32_t mode);
 int sli_model_get_exec(sli_model* m, int32_t* mode);
 /* One decode step (hipGraph replay; captured on first use). Asynchronous on the model's stream. */

@@ -33,7 +33,6 @@
 #include "persist.h"
 #include "rope_table.h"
 #include "step_state.h"
-#include "stream_engine.h"
 
 namespace sli {
 
@@ -115,12 +114,6 @@ struct sli_model {
     size_t ps_sync_bytes = 0;
     size_t ps_lds = 0;
     int ps_grid = 0;
-    // SLI_EXEC_STREAM (stream_engine.h): the whole step as one launch around an LDS-DMA weight ring
-    sli::EsArgs* es_args = nullptr;  // device copy of the args record
-    unsigned* es_edges = nullptr;    // arrival counters, zeroed by a memset node before each launch
-    size_t es_edges_bytes = 0;
-    sli::EsLds es_lds{};
-    int es_grid = 0;
 };
 
 // In-process tensor parallelism (the "fake communicator"): tp_size rank models on
@@ -238,95 +231,6 @@ static int ps_setup(sli_model* m) {
     SLI_HIP(hipMemcpy(dev, &a, sizeof(PsArgs), hipMemcpyHostToDevice));
     m->ps_args = dev;
     return ps_launch_model(m, true);
-}
-
-// ---------------------------------------------------------------- stream engine (stream_engine.h)
-static bool es_supported(const sli_model* m) {
-    const int g = m->hq / m->hkv;
-    return m->B == 1 && !m->partial && !m->group && (g == 1 || g == 2 || g == 4) && (m->hd == 64 || m->hd == 128);
-}
-
-// Allocate the hand-off buffers and the args record of the stream engine (once per model).
-static int es_setup(sli_model* m) {
-    if (m->es_args) return SLI_OK;
-    SLI_CHECK(m->B == 1, SLI_ERR_STATE, "stream engine: batch 1 only (batched decode runs the MFMA launches)");
-    SLI_CHECK(!m->partial && !m->group, SLI_ERR_STATE, "stream engine: tensor parallelism runs the launches");
-    SLI_CHECK(es_supported(m), SLI_ERR_STATE, "stream engine: heads per kv head must be 1, 2 or 4");
-    const int L = m->L, D = m->D, hd = m->hd, grid = device_cus();
-    EsArgs a{};
-    a.ppj = es_job_positions(m->c.kv_dtype, hd, m->hkv, m->T, grid);
-    a.max_splits = (m->T + a.ppj - 1) / a.ppj;
-    SLI_TRY(es_layout(D, m->Il, m->hq, hd, m->hkv, m->v_n, grid, &m->es_lds));
-    int rc = SLI_OK;
-    auto A = [&](void** p, size_t bytes) {
-        if (rc == SLI_OK) rc = model_alloc(m, p, bytes);
-    };
-    m->es_edges_bytes = sizeof(unsigned) * (size_t)(kEsOpsPerLayer * L + 1) * kEsShards * kEsShardWords;
-    A((void**)&m->es_edges, m->es_edges_bytes);
-    A((void**)&a.xv, sizeof(float) * (size_t)(2 * L + 1) * D);
-    A((void**)&a.qv, sizeof(float) * (size_t)L * m->hq * hd);
-    A((void**)&a.kvn, sizeof(float) * (size_t)L * 2 * m->hkv * hd);
-    A((void**)&a.part, sizeof(float) * (size_t)L * m->hq * a.max_splits * (hd + kAttnPartPad));
-    A((void**)&a.actv, sizeof(float) * (size_t)L * m->Il);
-    A((void**)&a.keys, sizeof(unsigned long long) * grid);
-    void* zero = nullptr;
-    A(&zero, 1024);
-    EsLayer* layers = nullptr;
-    A((void**)&layers, sizeof(EsLayer) * L);
-    EsArgs* dev = nullptr;
-    A((void**)&dev, sizeof(EsArgs));
-    if (rc != SLI_OK) return rc;
-    std::vector<EsLayer> hl(L);
-    for (int l = 0; l < L; ++l) {
-        const LayerW& w = m->layers[l];
-        hl[l] = EsLayer{w.qkv, w.qkv_s, w.wo, w.wo_s, w.gu, w.gu_s, w.down, w.down_s};
-    }
-    a.layers = layers;
-    a.emb = m->emb;
-    a.emb_s = m->emb_s;
-    a.norms = m->norms;
-    a.kc = m->kc;
-    a.vc = m->vc;
-    a.sin_t = m->sin_t;
-    a.cos_t = m->cos_t;
-    a.st = m->st;
-    a.prompt = m->prompt;
-    a.hist = m->hist;
-    a.logits = m->logits;
-    a.edges = m->es_edges;
-    a.zero = zero;
-    a.D = D;
-    a.L = L;
-    a.T = m->T;
-    a.hd = hd;
-    a.hq = m->hq;
-    a.hkv = m->hkv;
-    a.Il = m->Il;
-    a.V = m->V;
-    a.v_lo = m->v_lo;
-    a.v_n = m->v_n;
-    a.eps = m->c.eps;
-    a.scale = 1.0f / sqrtf((float)hd);  // mha_kernel.cpp:41
-    a.act_mode = m->c.act_mode;
-    a.slots = m->es_lds.slots;
-    a.lds_xs = m->es_lds.xs;
-    a.lds_res = m->es_lds.res;
-    a.lds_xres = m->es_lds.xres;
-    a.lds_ctl = m->es_lds.ctl;
-    SLI_HIP(hipMemset(zero, 0, 1024));
-    SLI_HIP(hipMemset(m->es_edges, 0, m->es_edges_bytes));
-    SLI_HIP(hipMemcpy(layers, hl.data(), sizeof(EsLayer) * L, hipMemcpyHostToDevice));
-    SLI_HIP(hipMemcpy(dev, &a, sizeof(EsArgs), hipMemcpyHostToDevice));
-    m->es_grid = grid;
-    SLI_TRY(es_launch(dev, m->c.w_dtype, m->c.kv_dtype, hd, m->hq / m->hkv, grid, m->es_lds.total, m->stream, 1));
-    m->es_args = dev;
-    return SLI_OK;
-}
-
-static int es_record(sli_model* m) {
-    SLI_HIP(hipMemsetAsync(m->es_edges, 0, m->es_edges_bytes, m->stream));
-    return es_launch(m->es_args, m->c.w_dtype, m->c.kv_dtype, m->hd, m->hq / m->hkv, m->es_grid, m->es_lds.total,
-                     m->stream, 0);
 }
 
 #define SLI_NCCL(expr)                                                                          \
@@ -823,7 +727,6 @@ struct StepRecorder {
 
     // one model and its own communicator (none, RCCL, or the debug modes)
     static int record(sli_model* m) {
-        if (m->exec == SLI_EXEC_STREAM) return es_record(m);
         if (m->exec == SLI_EXEC_PERSISTENT) {
             SLI_HIP(hipMemsetAsync(m->ps_sync, 0, m->ps_sync_bytes, m->stream));
             return ps_launch_model(m, false);
@@ -1058,7 +961,6 @@ static int check_device_errors(sli_model* m) {
     if (bits & kOsErrTimeout) m->os_dead = true;  // epochs may disagree across ranks from here on
     std::string why;
     if (bits & kPsErrTimeout) why += " persistent-step barrier timed out;";
-    if (bits & kEsErrTimeout) why += " stream-engine hand-off timed out;";
     if (bits & kOsErrTimeout) why += " one-shot all-reduce timed out (the one-shot path is now refused);";
     return fail(SLI_ERR_STATE, "device error bits 0x" + std::to_string(bits) + ":" + why + " outputs are stale");
 }
@@ -1542,11 +1444,9 @@ int sli_model_get_history(sli_model* m, int32_t seq, int32_t n, int32_t* out) {
 
 int sli_model_set_exec(sli_model* m, int32_t mode) {
     SLI_CHECK(m, SLI_ERR_ARG, "null model");
-    SLI_CHECK(mode == SLI_EXEC_LAUNCHES || mode == SLI_EXEC_PERSISTENT || mode == SLI_EXEC_STREAM, SLI_ERR_ARG,
-              "unknown execution mode");
+    SLI_CHECK(mode == SLI_EXEC_LAUNCHES || mode == SLI_EXEC_PERSISTENT, SLI_ERR_ARG, "unknown execution mode");
     SLI_HIP(hipSetDevice(m->c.device));
     if (mode == SLI_EXEC_PERSISTENT) SLI_TRY(ps_setup(m));
-    if (mode == SLI_EXEC_STREAM) SLI_TRY(es_setup(m));
     if (mode != m->exec) {  // re-capture the step graph on the next step
         SLI_HIP(hipStreamSynchronize(m->stream));
         if (m->graph_exec) (void)hipGraphExecDestroy(m->graph_exec);

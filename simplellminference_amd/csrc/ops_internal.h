@@ -22,18 +22,6 @@ struct PsArgs;
 int ps_max_splits(int kv_dtype, int hd, int T);
 int ps_launch(const PsArgs& a, const PsArgs* a_dev, int w_dtype, int kv_dtype, int grid, size_t lds, hipStream_t s, bool prepare);
 
-// stream engine (stream_engine.h / stream_engine.hip): the batch-1 step as one launch around an LDS-DMA
-// weight ring
-struct EsArgs;
-struct EsLds {
-    int slots, xs, res, xres, ctl, total;  // ring slots; LDS byte offsets; bytes
-};
-int es_positions_per_slot(int kv_dtype, int hd);
-int es_job_positions(int kv_dtype, int hd, int hkv, int T, int grid);
-int es_layout(int D, int Il, int hq, int hd, int hkv, int v_n, int grid, EsLds* out);
-int es_launch(const EsArgs* a_dev, int w_dtype, int kv_dtype, int hd, int g, int grid, size_t lds, hipStream_t s,
-              int mode);
-
 int embedding_launch(int token, const int32_t* token_dev, const void* table, int dtype, const float* row_scale,
                      float* out, int vocab, int dim, hipStream_t s);
 

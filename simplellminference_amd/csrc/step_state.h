@@ -11,12 +11,10 @@ struct DevState {
     int32_t n_forced;     // prompt length (teacher forcing while pos < n_forced)
     int32_t last_argmax;  // greedy argmax of the last step's logits
     int32_t advance;      // 1: finalize advances pos/token; 0: idempotent step (bench)
-    int32_t error;        // device-side error bits: kPsErrTimeout (persist.h), kOsErrTimeout (oneshot.h),
-                          // kEsErrTimeout (the stream engine); checked by every predict path
+    int32_t error;        // device-side error bits: kPsErrTimeout (persist.h), kOsErrTimeout (oneshot.h);
+                          // checked by every predict path
     unsigned long long key;  // argmax key of the last step (0 between steps)
 };
-
-constexpr int kEsErrTimeout = 8;  // DevState::error bit: a stream-engine hand-off wait gave up
 
 // model.cpp:157-183: next position; teacher-forced prompt token while inside the prompt, else greedy.
 __device__ __forceinline__ void finalize_state(DevState* st, const int32_t* prompt, int32_t* hist, int T) {

@@ -159,11 +159,10 @@ class LlamaModel:
         return max(0, min(chunk, c.vocab_size - self.tp_rank * chunk))
 
     # ------------------------------------------------------------------ execution
-    EXEC = {"launches": 0, "persistent": 1, "stream": 2}
+    EXEC = {"launches": 0, "persistent": 1}
 
     def set_exec(self, mode: str) -> "LlamaModel":
-        """"launches" (one graph of fused launches), "persistent" (the whole step as one launch, grid barriers
-        between phases) or "stream" (the whole step as one launch around an LDS-DMA weight ring)."""
+        """"launches" (one graph of fused launches) or "persistent" (the whole step as one launch)."""
         call("sli_model_set_exec", self._h, self.EXEC[mode])
         return self
 
