@@ -347,7 +347,8 @@ def main():
                                    "frac": round(tflops / 2500.0, 5)}
     if a.prefill_tokens > 1 and B == 1 and a.prefill_tokens <= a.ctx:
         progress("prefill")
-        # prompt prefill: positions 0..n-2 eight at a time through the MFMA projections
+        # prompt prefill: positions 0..n-2 in chunks of up to 256 through the MFMA GEMMs
+        # (prefill.h); the last prompt position is the first decode step (not part of this timing)
         n = a.prefill_tokens
         ids = [(1 + 7919 * i) % cfg.vocab_size for i in range(n)]
         model.prefill(ids)  # warm-up: capture + first run
@@ -359,15 +360,29 @@ def main():
         barrier()
         tp = (time.perf_counter() - tp) / reps
         wb_el = {"f16": 2.0, "i8": 1.0, "f32": 4.0}[a.w_dtype]
-        params = (wbytes - (4.0 * 0 if a.w_dtype != "i8" else 0.0)) / wb_el - cfg.vocab_size * cfg.hidden_size / world
-        steps = -(-(n - 1) // 8)
-        flops = 2.0 * params * 8 * steps  # every lane of every chunk, the padding lanes included
-        out["prefill"] = {"prompt_tokens": n, "positions_prefilled": n - 1, "chunk_steps": steps,
+        layer_bytes = wbytes - cfg.vocab_size * cfg.hidden_size * wb_el / world  # this rank's layer weights
+        params = layer_bytes / wb_el
+        mfma = a.w_dtype in ("f16", "i8")
+        chunks = []  # (valid rows, padded rows) per chunk (engine.hip kPfSizes)
+        for p0 in range(0, n - 1, 256):
+            nv = min(256, n - 1 - p0)
+            chunks.append((nv, next(m for m in (32, 64, 128, 256) if nv <= m)))
+        # weight passes: the qkv / gate-up GEMMs read a weight row once per min(M, 128) rows, wo / down once
+        # per min(M, 64) (engine.hip pf_bm); qkv + gate-up are ~2/3 of a Llama layer's weights
+        passes = sum((2.0 / 3.0) * (M // min(M, 128)) + (1.0 / 3.0) * (M // min(M, 64)) for _, M in chunks)
+        useful = 2.0 * params * (n - 1) * world  # whole-job flops of the projections (1 flop per MAC x 2)
+        issued = 4.0 * params * sum(M for _, M in chunks) * world  # hi + lo MFMAs over the padded rows
+        out["prefill"] = {"prompt_tokens": n, "positions_prefilled": n - 1,
+                          "chunks": [{"rows": nv, "padded": M} for nv, M in chunks],
                           "seconds": round(tp, 5), "tokens_per_s": round((n - 1) / tp, 1),
-                          "weight_bytes_streamed": round(steps * (wbytes - cfg.vocab_size * cfg.hidden_size * wb_el)),
-                          "mfma_tflops": round(flops / tp / 1e12, 2), "mfma_peak_tflops": 2500.0,
-                          "path": ("MFMA bgemm (v_mfma_f32_16x16x32_f16), 8 positions per step" if a.w_dtype == "f16"
-                                   and world == 1 else "decode step, teacher-forced (no MFMA path for this config)"),
+                          "weight_passes": round(passes, 2) if mfma else n - 1,
+                          "weight_bytes_streamed": round((passes if mfma else n - 1) * layer_bytes * world),
+                          "projection_tflops": round(useful / tp / 1e12, 2),
+                          "mfma_issued_tflops": round(issued / tp / 1e12, 2) if mfma else None,
+                          "mfma_peak_tflops": 2500.0,
+                          "path": ("MFMA pgemm (v_mfma_f32_16x16x32_f16, fp16 hi + lo activations), chunks of "
+                                   "<= 256 positions, block-causal attention" if mfma
+                                   else "decode step, teacher-forced (no MFMA path for fp32 weights)"),
                           "vs_token_by_token_s": round((n - 1) * ms * 1e-3, 4)}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a.cpu_seconds, a.preset, a.ctx)

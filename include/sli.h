@@ -186,9 +186,11 @@ int sli_model_set_state_seq(sli_model* m, int32_t seq, int32_t token, int32_t po
 int sli_model_set_prompt_seq(sli_model* m, int32_t seq, const int32_t* ids, int32_t n);
 int sli_model_get_state_seq(sli_model* m, int32_t seq, int32_t* pos, int32_t* token, int32_t* last_argmax,
                             int32_t* error);
-/* Prompt prefill (batch-1 models): positions 0 .. n-2 of the prompt run through the layers kPfLanes = 8 at a
- * time, the projections as an MFMA skinny GEMM over the positions (fp16 weights, no tensor parallelism;
- * otherwise through the decode step, teacher-forced), filling the K/V cache; the state is left at
+/* Prompt prefill (batch-1 models): positions 0 .. n-2 of the prompt run through the layers in chunks of up
+ * to 256 positions, every projection one MFMA GEMM over the chunk and attention block-causal over the
+ * cache (fp16 / int8 weights, head_dim 64 / 128; otherwise through the decode step, teacher-forced; under
+ * multi-process tensor parallelism every rank calls it, the chunk's residual rows all-reduced over RCCL
+ * twice per layer), filling the K/V cache; the state is left at
  * (token ids[n-1], position n-1, advancing, prompt = ids), so the next sli_model_step yields the first
  * greedy token exactly as the reference's token-by-token predict (model.cpp:157-165) would. */
 int sli_model_prefill(sli_model* m, const int32_t* ids, int32_t n);
@@ -248,6 +250,12 @@ int sli_tp_group_sync(sli_tp_group* g);
  * [max_length][batch][vocab] with the ranks' vocab shards in place (the full vocabulary). */
 int sli_tp_group_predict_batch(sli_tp_group* g, const int32_t* prompts, const int32_t* lens, int32_t ld,
                                int32_t max_length, int32_t* tokens_out, float* logits_out);
+/* sli_model_prefill / sli_model_predict_prefill over the group (batch-1 groups): the ranks' prefill chunks
+ * run in lockstep, the residual rows summed over the ranks after every wo and down GEMM. logits_out
+ * [max_length][vocab] (rows < n_prompt - 1 NaN). */
+int sli_tp_group_prefill(sli_tp_group* g, const int32_t* ids, int32_t n);
+int sli_tp_group_predict_prefill(sli_tp_group* g, const int32_t* prompt, int32_t n_prompt, int32_t max_length,
+                                 int32_t* tokens_out, float* logits_out);
 
 /* Roofline probe: replays the step's weight-streaming (GEMV) kernels `iters` times between HIP events
  * on the model's stream; returns mean device time per GEMV launch, algorithmic bytes per launch and

@@ -117,6 +117,8 @@ _SIGS = {
     "sli_tp_group_step": (c_int, [c_vp]),
     "sli_tp_group_sync": (c_int, [c_vp]),
     "sli_tp_group_predict_batch": (c_int, [c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp]),
+    "sli_tp_group_prefill": (c_int, [c_vp, c_vp, c_i32]),
+    "sli_tp_group_predict_prefill": (c_int, [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp]),
 }
 
 _lib = None

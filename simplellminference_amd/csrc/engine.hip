@@ -31,6 +31,7 @@
 #include "oneshot.h"
 #include "ops_internal.h"
 #include "persist.h"
+#include "prefill.h"
 #include "rope_table.h"
 #include "step_state.h"
 
@@ -86,17 +87,15 @@ struct sli_model {
     unsigned* bg_cnt = nullptr;           // their arrival counters (zero between launches)
     unsigned long long* bkeys = nullptr;  // [B] per-sequence argmax keys (all-reduced MAX under TP)
     int key_ld = 0;                       // per-sequence stride of the per-workgroup argmax keys
-    // prompt prefill (sli_model_prefill): kPfLanes prompt positions of this one sequence per step, the
-    // projections on MFMA (bgemm.h), every lane writing its K/V row into the model's own cache
+    // prompt prefill (sli_model_prefill, prefill.h): chunks of up to kPfMaxChunk prompt positions through
+    // every layer per weight pass; one captured graph per chunk size (kPfSizes)
     struct Prefill {
-        float *x = nullptr, *q = nullptr, *attn = nullptr, *act = nullptr, *part = nullptr;
-        unsigned* attn_count = nullptr;
-        sli::DevState* st = nullptr;  // [kPfLanes]: lane b feeds token st[b].token at position st[b].pos
-        float* ws = nullptr;
-        unsigned* cnt = nullptr;
-        sli::BgPlan qkv, wo, gu, down;
-        hipGraph_t graph = nullptr;
-        hipGraphExec_t exec = nullptr;
+        float *x = nullptr, *xpart = nullptr, *q = nullptr;  // [chunk][D], [chunk][D] (TP partials), [chunk][hq hd]
+        __half *hhi = nullptr, *hlo = nullptr;  // [chunk][max(D, hq hd)]: normed x / attention out, fp16 hi + lo
+        __half *ahi = nullptr, *alo = nullptr;  // [chunk][Il]: SwiGLU out, fp16 hi + lo
+        sli::PfState* ps = nullptr;             // chunk start position + valid rows (device)
+        hipGraph_t graph[4] = {};
+        hipGraphExec_t exec[4] = {};
     } pf;
     // tensor-parallel all-reduce: SLI_ALLREDUCE_RCCL (ncclAllReduce) or SLI_ALLREDUCE_ONESHOT (oneshot.h)
     int ar_mode = SLI_ALLREDUCE_RCCL;
@@ -121,7 +120,7 @@ struct sli_model {
 // device-side reduction over the ranks' buffers in rank order (the ranks' kernels are the multi-GPU
 // ones, so the sharded engine itself is what the group tests run).
 constexpr int kMaxGroup = 8;
-constexpr int kPfLanes = 8;  // prompt positions per prefill step (the MFMA projection's batch limit)
+constexpr int kPfSizes[4] = {32, 64, 128, 256};  // prefill chunk sizes (the last is prefill.h kPfMaxChunk)
 struct sli_tp_group {
     int n = 0;
     int device = 0;
@@ -129,6 +128,8 @@ struct sli_tp_group {
     std::vector<sli_model*> ranks;
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
+    hipGraph_t pf_graph[4] = {};  // the ranks' prefill chunks in lockstep, per chunk size
+    hipGraphExec_t pf_exec[4] = {};
 };
 
 namespace sli {
@@ -783,60 +784,109 @@ struct StepRecorder {
         SLI_HIP(hipGetLastError());
         return SLI_OK;
     }
-    // ---- prompt prefill (model.cpp:157-165 runs the prompt one token per forward): one step runs the
-    // layers for kPfLanes prompt positions of the one sequence at once — the projections as an MFMA
-    // skinny GEMM over the lanes (weights read once per kPfLanes positions), attention per lane over the
-    // shared cache up to the lane's own position (lane b sees the rows lanes < b wrote in the same qkv
-    // launch), K/V rows written where the decode step writes them. No LM head: the prompt's logits are
-    // not used (teacher forcing); the last prompt position runs as an ordinary decode step.
-    static BgIn bin_pf(sli_model* m, const float* x, const float* norm, int K) {
-        BgIn in{};
-        in.x = x;
-        in.norm_w = norm;
-        in.eps = m->c.eps;
-        in.K = K;
-        in.B = kPfLanes;
-        in.ws = m->pf.ws;
-        in.counters = m->pf.cnt;
-        return in;
-    }
-    static int prepare_prefill(sli_model* m) {
-        SLI_TRY((allow<BgEpiQKV<KT>, true>(m)));
-        SLI_TRY((allow<BgEpiStore, false>(m)));
-        SLI_TRY((allow<BgEpiSwiGLU, true>(m)));
-        return SLI_OK;
-    }
-    static int record_prefill(sli_model* m) {
-        if constexpr (!std::is_same<WT, __half>::value) {
-            return fail(SLI_ERR_ARG, "prefill needs fp16 weights");
+    // ---- prompt prefill (model.cpp:157-165 runs the prompt one token per forward; prefill.h): a chunk of
+    // M prompt positions runs through every layer together, each projection one MFMA GEMM over the chunk
+    // (weights read once per BM positions), attention block-causal over the cache rows the chunk's own qkv
+    // GEMM just wrote. No LM head: the prompt's logits are not used (teacher forcing); the last prompt
+    // position runs as an ordinary decode step. Phases as record_phase: 2l = qkv, attention, wo; 2l+1 =
+    // gate/up, down; under tensor parallelism each ends with the all-reduce of the chunk's residual rows.
+    static int pf_bm(int M, bool out) { return std::min(M, out ? 64 : 128); }
+    template <class Epi, int BM>
+    static int pg_bm(sli_model* m, const void* W, int N, int K, const __half* hi, const __half* lo, const Epi& e,
+                     int M) {
+        if constexpr (std::is_same<WT, float>::value) {
+            return fail(SLI_ERR_ARG, "prefill needs fp16 or int8 weights");
         } else {
-            auto& p = m->pf;
-            hipStream_t s = m->stream;
-            const int eb = std::min(64, (m->D + 255) / 256);
-            hipLaunchKernelGGL(embedding_batch_kernel<WT>, dim3(eb, kPfLanes), dim3(256), 0, s, p.st, (const WT*)m->emb,
-                               m->emb_s, p.x, m->V, m->D);
-            SLI_HIP(hipGetLastError());
-            const long long ls = (long long)m->hkv * m->T * m->hd;
-            for (int l = 0; l < m->L; ++l) {
-                const LayerW& w = m->layers[l];
-                KT* kc = (KT*)m->kc + (size_t)l * ls;
-                KT* vc = (KT*)m->vc + (size_t)l * ls;
-                BgEpiQKV<KT> eq{p.q, kc, vc, &p.st->pos, kPosStride, m->sin_t, m->cos_t, m->hq, m->hkv, m->hd, m->T};
-                eq.kv_seq = 0;  // every lane writes this sequence's cache
-                SLI_TRY(bg(m, w.qkv, bin_pf(m, p.x, m->norms + (size_t)(2 * l) * m->D, m->D), eq, p.qkv));
-                // lane b's kv heads [b*hkv, (b+1)*hkv) read cache heads [0, hkv) up to lane b's position
-                SLI_TRY(mha_launch<KT>(p.q, (const KT*)m->kc, (const KT*)m->vc, p.attn, l, 0, &p.st->pos, m->T, m->hd,
-                                       kPfLanes * m->hq, kPfLanes * m->hkv, m->hd, (long long)m->T * m->hd, ls, p.part,
-                                       p.attn_count, s, m->hkv, kPosStride, m->hkv));
-                BgEpiStore eo{p.x, p.x, nullptr, 1.0f, m->D, m->D};
-                SLI_TRY(bg(m, w.wo, bin_pf(m, p.attn, nullptr, m->hq * m->hd), eo, p.wo));
-                BgEpiSwiGLU eg{p.act, m->Il, m->c.act_mode};
-                SLI_TRY(bg(m, w.gu, bin_pf(m, p.x, m->norms + (size_t)(2 * l + 1) * m->D, m->D), eg, p.gu));
-                BgEpiStore ed{p.x, p.x, nullptr, 1.0f, m->D, m->D};
-                SLI_TRY(bg(m, w.down, bin_pf(m, p.act, nullptr, m->Il), ed, p.down));
-            }
+            const PgIn<WT> in{(const WT*)W, hi, lo, N, K, M};
+            SLI_HIP((launch_pgemm<Epi, BM, WT>(in, e, m->pf.ps, m->stream)));
             return SLI_OK;
         }
+    }
+    template <class Epi>
+    static int pg(sli_model* m, const void* W, int N, int K, const __half* hi, const __half* lo, const Epi& e, int M,
+                  int BM) {
+        if (BM == 32) return pg_bm<Epi, 32>(m, W, N, K, hi, lo, e, M);
+        if (BM == 64) return pg_bm<Epi, 64>(m, W, N, K, hi, lo, e, M);
+        return pg_bm<Epi, 128>(m, W, N, K, hi, lo, e, M);
+    }
+    template <class Epi>
+    static int allow_pg(sli_model*) {
+        if constexpr (!std::is_same<WT, float>::value) {
+            SLI_HIP((pgemm_allow_lds<Epi, 32, WT>()));
+            SLI_HIP((pgemm_allow_lds<Epi, 64, WT>()));
+            SLI_HIP((pgemm_allow_lds<Epi, 128, WT>()));
+        }
+        return SLI_OK;
+    }
+    static int prepare_prefill(sli_model* m) {
+        SLI_TRY(allow_pg<PgEpiQKV<KT>>(m));
+        SLI_TRY(allow_pg<PgEpiResid>(m));
+        SLI_TRY(allow_pg<PgEpiSwiGLU>(m));
+        return SLI_OK;
+    }
+    static int record_pf_phase(sli_model* m, int p, int M) {
+        auto& f = m->pf;
+        hipStream_t s = m->stream;
+        const int D = m->D, hd = m->hd, QD = m->hq * hd;
+        if (p == 0) {
+            hipLaunchKernelGGL(pf_embed_kernel<WT>, dim3(M), dim3(256), 0, s, f.ps, m->prompt, (const WT*)m->emb,
+                               m->emb_s, f.x, D);
+            SLI_HIP(hipGetLastError());
+        }
+        const int l = p / 2;
+        const LayerW& w = m->layers[l];
+        const bool tp = m->partial;
+        PgEpiResid er{tp ? f.xpart : f.x, (!tp || m->c.tp_rank == 0) ? f.x : nullptr, nullptr, D, D};
+        hipLaunchKernelGGL(pf_norm_split_kernel, dim3(M), dim3(256), 0, s, f.x, m->norms + (size_t)p * D, f.hhi, f.hlo,
+                           D, m->c.eps);
+        SLI_HIP(hipGetLastError());
+        if (p % 2 == 0) {
+            const size_t ls = (size_t)l * m->hkv * m->T * hd;
+            PgEpiQKV<KT> eq{f.q, (KT*)m->kc + ls, (KT*)m->vc + ls, w.qkv_s, m->sin_t, m->cos_t, m->hq, m->hkv, hd, m->T};
+            SLI_TRY(pg(m, w.qkv, (m->hq + 2 * m->hkv) * hd, D, f.hhi, f.hlo, eq, M, pf_bm(M, false)));
+            PfAttnArgs<KT> aa{f.q, (const KT*)m->kc + ls, (const KT*)m->vc + ls, f.hhi, f.hlo, m->hq, m->hkv, m->T,
+                              1.0f / sqrtf((float)hd)};
+            const dim3 ag((M + kPaQB - 1) / kPaQB, m->hq);
+            if (hd == 128)
+                hipLaunchKernelGGL((pf_attn_kernel<KT, 128>), ag, dim3(256), 0, s, aa, f.ps);
+            else
+                hipLaunchKernelGGL((pf_attn_kernel<KT, 64>), ag, dim3(256), 0, s, aa, f.ps);
+            SLI_HIP(hipGetLastError());
+            er.rscale = w.wo_s;
+            return pg(m, w.wo, D, QD, f.hhi, f.hlo, er, M, pf_bm(M, true));
+        }
+        PgEpiSwiGLU eg{f.ahi, f.alo, w.gu_s, m->Il, m->c.act_mode};
+        SLI_TRY(pg(m, w.gu, 2 * m->Il, D, f.hhi, f.hlo, eg, M, pf_bm(M, false)));
+        er.rscale = w.down_s;
+        return pg(m, w.down, D, m->Il, f.ahi, f.alo, er, M, pf_bm(M, true));
+    }
+    static int record_prefill(sli_model* m, int M) {
+        for (int p = 0; p < 2 * m->L; ++p) {
+            SLI_TRY(record_pf_phase(m, p, M));
+            const size_t n = (size_t)M * m->D;
+            if (m->collectives)
+                SLI_NCCL(ncclAllReduce(m->pf.xpart, m->pf.x, n, ncclFloat32, ncclSum, m->comm, m->stream));
+            else if (m->partial)  // debug no-comm mode: keep the local partial as the residual stream
+                SLI_HIP(hipMemcpyAsync(m->pf.x, m->pf.xpart, sizeof(float) * n, hipMemcpyDeviceToDevice, m->stream));
+        }
+        return SLI_OK;
+    }
+    static int record_group_prefill(sli_tp_group* g, int M) {
+        sli_model* m0 = g->ranks[0];
+        GroupSumArgs sa{};
+        sa.n_ranks = g->n;
+        sa.n = M * m0->D;
+        for (int r = 0; r < g->n; ++r) {
+            sa.src[r] = g->ranks[r]->pf.xpart;
+            sa.dst[r] = g->ranks[r]->pf.x;
+        }
+        const int blocks = std::min(256, (sa.n + 255) / 256);
+        for (int p = 0; p < 2 * m0->L; ++p) {
+            for (int r = 0; r < g->n; ++r) SLI_TRY(record_pf_phase(g->ranks[r], p, M));
+            hipLaunchKernelGGL(group_sum_kernel, dim3(blocks), dim3(256), 0, g->stream, sa);
+            SLI_HIP(hipGetLastError());
+        }
+        return SLI_OK;
     }
     // All weight-streaming launches of one step (for the roofline probe).
     static int gemvs(sli_model* m) {
@@ -971,8 +1021,10 @@ static void destroy(sli_model* m) {
     if (m->stream) (void)hipStreamSynchronize(m->stream);
     if (m->graph_exec) (void)hipGraphExecDestroy(m->graph_exec);
     if (m->graph) (void)hipGraphDestroy(m->graph);
-    if (m->pf.exec) (void)hipGraphExecDestroy(m->pf.exec);
-    if (m->pf.graph) (void)hipGraphDestroy(m->pf.graph);
+    for (int b = 0; b < 4; ++b) {
+        if (m->pf.exec[b]) (void)hipGraphExecDestroy(m->pf.exec[b]);
+        if (m->pf.graph[b]) (void)hipGraphDestroy(m->pf.graph[b]);
+    }
     if (m->comm) ncclCommDestroy(m->comm);
     for (int r = 0; r < sli::kOsMaxRanks; ++r)
         if (m->os_peer[r] && m->os_peer[r] != m->os_buf) (void)hipIpcCloseMemHandle(m->os_peer[r]);
@@ -1309,51 +1361,51 @@ static int get_state(sli_model* m, int seq, int32_t* pos, int32_t* token, int32_
 }  // extern "C" (reopened below)
 
 // ---------------------------------------------------------------- prompt prefill
-// MFMA prefill needs fp16 weights, batch 1 and no tensor parallelism; otherwise the prompt runs through the
-// decode step itself (teacher forcing), which gives the same tokens.
+// The GEMM prefill (prefill.h) needs fp16 or int8 weights, batch 1, head_dim 64 or 128 and 64-multiple
+// projection depths; otherwise the prompt runs through the decode step itself (teacher forcing), which gives
+// the same tokens.
 static bool pf_supported(const sli_model* m) {
-    return m->c.w_dtype == SLI_DT_F16 && m->B == 1 && !m->partial && !m->group && m->D % 32 == 0 &&
-           m->Il % 32 == 0 && (m->hq * m->hd) % 32 == 0 && m->D <= kBgMaxStageK;
+    return m->c.w_dtype != SLI_DT_F32 && m->B == 1 && (m->hd == 64 || m->hd == 128) && m->D % 64 == 0 &&
+           m->Il % 64 == 0 && (m->hq * m->hd) % 64 == 0;
 }
 
-static int pf_setup(sli_model* m) {
+static int pf_bucket(int nv) {
+    for (int b = 0; b < 3; ++b)
+        if (nv <= kPfSizes[b]) return b;
+    return 3;
+}
+
+static int pf_alloc(sli_model* m) {
     auto& p = m->pf;
-    if (p.exec) return SLI_OK;
-    const int B = kPfLanes, D = m->D, hd = m->hd, cus = device_cus();
-    p.qkv = bg_plan((m->hq + 2 * m->hkv) * hd / 16, D, B, true, cus);
-    p.wo = bg_plan((D + 15) / 16, m->hq * hd, B, false, cus);
-    p.gu = bg_plan(m->Il / 8, D, B, true, cus);
-    p.down = bg_plan((D + 15) / 16, m->Il, B, false, cus);
-    size_t part = 0;
-    int groups = 1;
-    for (const BgPlan* q : {&p.qkv, &p.wo, &p.gu, &p.down}) {
-        if (q->groups <= 0) return fail(SLI_ERR_SHAPE, "prefill: no tiling fits");
-        part = std::max(part, bg_part_bytes(*q));
-        groups = std::max(groups, q->groups);
-    }
+    if (p.x) return SLI_OK;
+    const size_t M = kPfMaxChunk, D = m->D, QD = (size_t)m->hq * m->hd;
     int rc = SLI_OK;
     auto A = [&](void** ptr, size_t bytes) {
         if (rc == SLI_OK) rc = model_alloc(m, ptr, bytes);
     };
-    A((void**)&p.x, sizeof(float) * B * D);
-    A((void**)&p.q, sizeof(float) * B * m->hq * hd);
-    A((void**)&p.attn, sizeof(float) * B * m->hq * hd);
-    A((void**)&p.act, sizeof(float) * B * m->Il);
-    A((void**)&p.part, mha_part_bytes(m->T, B * m->hq, hd));
-    A((void**)&p.attn_count, sizeof(unsigned) * B * m->hkv);
-    A((void**)&p.st, sizeof(DevState) * B);
-    A((void**)&p.ws, part + 256);
-    A((void**)&p.cnt, sizeof(unsigned) * groups);
+    A((void**)&p.x, sizeof(float) * M * D);
+    if (m->partial) A((void**)&p.xpart, sizeof(float) * M * D);
+    A((void**)&p.q, sizeof(float) * M * QD);
+    A((void**)&p.hhi, sizeof(__half) * M * std::max(D, QD));
+    A((void**)&p.hlo, sizeof(__half) * M * std::max(D, QD));
+    A((void**)&p.ahi, sizeof(__half) * M * m->Il);
+    A((void**)&p.alo, sizeof(__half) * M * m->Il);
+    A((void**)&p.ps, sizeof(PfState));
     if (rc != SLI_OK) return rc;
-    SLI_HIP(hipMemset(p.attn_count, 0, sizeof(unsigned) * B * m->hkv));
-    SLI_HIP(hipMemset(p.cnt, 0, sizeof(unsigned) * groups));
-    SLI_TRY(SLI_DISPATCH(m, prepare_prefill, m));
-    return capture_graph(m->stream, p.graph, p.exec, [&]() { return SLI_DISPATCH(m, record_prefill, m); });
+    return SLI_DISPATCH(m, prepare_prefill, m);
+}
+
+// chunk c of the prompt's n - 1 prefilled positions
+static std::vector<PfState> pf_chunks(int n) {
+    std::vector<PfState> cs;
+    for (int p0 = 0; p0 < n - 1; p0 += kPfMaxChunk) cs.push_back(PfState{p0, std::min(kPfMaxChunk, n - 1 - p0)});
+    return cs;
 }
 
 extern "C" int sli_model_prefill(sli_model* m, const int32_t* ids, int32_t n) {
     SLI_CHECK(m && ids, SLI_ERR_ARG, "null argument");
     SLI_CHECK(m->B == 1, SLI_ERR_STATE, "prefill: batch-1 models (a batch prefills through predict_batch)");
+    SLI_CHECK(!m->group, SLI_ERR_STATE, "prefill: ranks of an in-process group prefill through sli_tp_group_prefill");
     SLI_CHECK(n >= 1 && n <= m->T, SLI_ERR_RANGE, "prompt length out of range");
     for (int i = 0; i < n; ++i)
         SLI_CHECK(ids[i] >= 0 && ids[i] < m->V, SLI_ERR_RANGE, "Token index is greater than vocab size.");
@@ -1361,22 +1413,16 @@ extern "C" int sli_model_prefill(sli_model* m, const int32_t* ids, int32_t n) {
     SLI_TRY(set_prompt(m, 0, ids, n));
     SLI_HIP(hipMemcpyAsync(m->hist, ids, sizeof(int32_t) * n, hipMemcpyHostToDevice, m->stream));
     if (n > 1 && pf_supported(m)) {
-        SLI_TRY(pf_setup(m));
-        // every chunk's lane states up front (positions 0 .. n-2; padding lanes repeat the last one): each
-        // chunk's copy reads host memory of its own, so the chunks are enqueued back to back, stream-ordered
-        const int steps = (n - 1 + kPfLanes - 1) / kPfLanes;
-        std::vector<DevState> lanes((size_t)steps * kPfLanes);
-        for (int c = 0; c < steps; ++c)
-            for (int b = 0; b < kPfLanes; ++b) {
-                const int p = std::min(c * kPfLanes + b, n - 2);
-                DevState& d = lanes[(size_t)c * kPfLanes + b];
-                d.pos = p;
-                d.token = ids[p];
-            }
-        for (int c = 0; c < steps; ++c) {
-            SLI_HIP(hipMemcpyAsync(m->pf.st, lanes.data() + (size_t)c * kPfLanes, sizeof(DevState) * kPfLanes,
-                                   hipMemcpyHostToDevice, m->stream));
-            SLI_HIP(hipGraphLaunch(m->pf.exec, m->stream));
+        SLI_TRY(pf_alloc(m));
+        const std::vector<PfState> cs = pf_chunks(n);
+        for (const PfState& c : cs) {  // capture before anything is enqueued behind the capture
+            const int b = pf_bucket(c.nv);
+            SLI_TRY(capture_graph(m->stream, m->pf.graph[b], m->pf.exec[b],
+                                  [&]() { return SLI_DISPATCH(m, record_prefill, m, kPfSizes[b]); }));
+        }
+        for (const PfState& c : cs) {  // each copy reads its own element of cs: enqueued back to back
+            SLI_HIP(hipMemcpyAsync(m->pf.ps, &c, sizeof(PfState), hipMemcpyHostToDevice, m->stream));
+            SLI_HIP(hipGraphLaunch(m->pf.exec[pf_bucket(c.nv)], m->stream));
         }
         SLI_HIP(hipStreamSynchronize(m->stream));
     } else {
@@ -1387,6 +1433,40 @@ extern "C" int sli_model_prefill(sli_model* m, const int32_t* ids, int32_t n) {
     }
     // the last prompt position is an ordinary decode step: it yields the first greedy token
     return set_state(m, 0, ids[n - 1], n - 1, 1);
+}
+
+extern "C" int sli_tp_group_prefill(sli_tp_group* g, const int32_t* ids, int32_t n) {
+    SLI_CHECK(g && ids, SLI_ERR_ARG, "null argument");
+    sli_model* m0 = g->ranks[0];
+    SLI_CHECK(m0->B == 1, SLI_ERR_STATE, "prefill: batch-1 groups (a batch prefills through predict_batch)");
+    SLI_CHECK(n >= 1 && n <= m0->T, SLI_ERR_RANGE, "prompt length out of range");
+    SLI_HIP(hipSetDevice(g->device));
+    for (sli_model* m : g->ranks) {
+        SLI_TRY(set_prompt(m, 0, ids, n));
+        SLI_HIP(hipMemcpyAsync(m->hist, ids, sizeof(int32_t) * n, hipMemcpyHostToDevice, m->stream));
+    }
+    if (n > 1 && pf_supported(m0)) {
+        for (sli_model* m : g->ranks) SLI_TRY(pf_alloc(m));
+        const std::vector<PfState> cs = pf_chunks(n);
+        for (const PfState& c : cs) {
+            const int b = pf_bucket(c.nv);
+            SLI_TRY(capture_graph(g->stream, g->pf_graph[b], g->pf_exec[b],
+                                  [&]() { return SLI_DISPATCH(m0, record_group_prefill, g, kPfSizes[b]); }));
+        }
+        for (const PfState& c : cs) {
+            for (sli_model* m : g->ranks)
+                SLI_HIP(hipMemcpyAsync(m->pf.ps, &c, sizeof(PfState), hipMemcpyHostToDevice, g->stream));
+            SLI_HIP(hipGraphLaunch(g->pf_exec[pf_bucket(c.nv)], g->stream));
+        }
+        SLI_HIP(hipStreamSynchronize(g->stream));
+    } else {
+        for (int p = 0; p < n - 1; ++p) {
+            for (sli_model* m : g->ranks) SLI_TRY(set_state(m, 0, ids[p], p, 0));
+            SLI_TRY(sli_tp_group_step(g));
+        }
+    }
+    for (sli_model* m : g->ranks) SLI_TRY(set_state(m, 0, ids[n - 1], n - 1, 1));
+    return SLI_OK;
 }
 
 extern "C" int sli_model_predict_prefill(sli_model* m, const int32_t* prompt, int32_t n_prompt, int32_t max_length,
@@ -1940,6 +2020,10 @@ int sli_tp_group_destroy(sli_tp_group* g) {
     if (g->stream) (void)hipStreamSynchronize(g->stream);
     if (g->exec) (void)hipGraphExecDestroy(g->exec);
     if (g->graph) (void)hipGraphDestroy(g->graph);
+    for (int b = 0; b < 4; ++b) {
+        if (g->pf_exec[b]) (void)hipGraphExecDestroy(g->pf_exec[b]);
+        if (g->pf_graph[b]) (void)hipGraphDestroy(g->pf_graph[b]);
+    }
     for (sli_model* m : g->ranks) destroy(m);
     if (g->stream) (void)hipStreamDestroy(g->stream);
     delete g;
@@ -1964,6 +2048,30 @@ int sli_tp_group_step(sli_tp_group* g) {
 int sli_tp_group_sync(sli_tp_group* g) {
     SLI_CHECK(g, SLI_ERR_ARG, "null group");
     SLI_HIP(hipStreamSynchronize(g->stream));
+    return SLI_OK;
+}
+
+int sli_tp_group_predict_prefill(sli_tp_group* g, const int32_t* prompt, int32_t n_prompt, int32_t max_length,
+                                 int32_t* tokens_out, float* logits_out) {
+    SLI_CHECK(g && prompt && tokens_out, SLI_ERR_ARG, "null argument");
+    sli_model* m0 = g->ranks[0];
+    SLI_CHECK(max_length >= n_prompt && max_length <= m0->T, SLI_ERR_RANGE,
+              "max_length must be in [n_prompt, max_len]");
+    SLI_TRY(sli_tp_group_prefill(g, prompt, n_prompt));
+    const size_t V = (size_t)m0->V;
+    if (logits_out)
+        for (size_t i = 0; i < (size_t)(n_prompt - 1) * V; ++i) logits_out[i] = NAN;
+    for (int t = n_prompt - 1; t < max_length; ++t) {
+        SLI_TRY(sli_tp_group_step(g));
+        if (!logits_out) continue;
+        for (sli_model* m : g->ranks)
+            SLI_HIP(hipMemcpyAsync(logits_out + (size_t)t * V + m->v_lo, m->logits, sizeof(float) * m->v_n,
+                                   hipMemcpyDeviceToHost, g->stream));
+        SLI_HIP(hipStreamSynchronize(g->stream));
+    }
+    SLI_HIP(hipMemcpyAsync(tokens_out, m0->hist, sizeof(int32_t) * max_length, hipMemcpyDeviceToHost, g->stream));
+    SLI_HIP(hipStreamSynchronize(g->stream));
+    for (sli_model* m : g->ranks) SLI_TRY(check_device_errors(m));
     return SLI_OK;
 }
 

@@ -227,8 +227,9 @@ class LlamaModel:
         return (toks, logits) if want_logits else toks
 
     def prefill(self, prompt_ids):
-        """Run prompt positions 0..n-2 through the layers 8 at a time (MFMA projections) and leave the state at
-        the last prompt token, so the next step() yields the first greedy token (sli_model_prefill)."""
+        """Run prompt positions 0..n-2 through the layers in chunks of up to 256 (MFMA GEMM projections,
+        block-causal attention) and leave the state at the last prompt token, so the next step() yields the
+        first greedy token (sli_model_prefill). Under multi-process tensor parallelism every rank calls it."""
         p = np.ascontiguousarray(prompt_ids, np.int32)
         call("sli_model_prefill", self._h, p.ctypes.data_as(ctypes.c_void_p), p.size)
 
@@ -408,6 +409,20 @@ class TPGroup:
              lens.ctypes.data_as(ctypes.c_void_p), ld, max_length, toks.ctypes.data_as(ctypes.c_void_p),
              logits.ctypes.data_as(ctypes.c_void_p) if want_logits else None)
         return (toks, logits.transpose(1, 0, 2).copy()) if want_logits else toks
+
+    def prefill(self, prompt_ids):
+        """sli_tp_group_prefill: the ranks' prefill chunks in lockstep (batch-1 groups)."""
+        p = np.ascontiguousarray(prompt_ids, np.int32)
+        call("sli_tp_group_prefill", self._g, p.ctypes.data_as(ctypes.c_void_p), p.size)
+
+    def predict_prefill(self, prompt_ids, max_length: int, want_logits: bool = False):
+        """predict() with the prompt prefilled; logits [max_length, vocab], rows < len(prompt) - 1 NaN."""
+        p = np.ascontiguousarray(prompt_ids, np.int32)
+        toks = np.empty(max_length, np.int32)
+        logits = np.empty((max_length, self.config.vocab_size), np.float32) if want_logits else None
+        call("sli_tp_group_predict_prefill", self._g, p.ctypes.data_as(ctypes.c_void_p), p.size, max_length,
+             toks.ctypes.data_as(ctypes.c_void_p), logits.ctypes.data_as(ctypes.c_void_p) if want_logits else None)
+        return (toks, logits) if want_logits else toks
 
     def predict(self, prompt_ids, max_length: int, want_logits: bool = False):
         r = self.predict_batch([list(prompt_ids)] * self.batch, max_length, want_logits)
