@@ -367,16 +367,26 @@ def main():
         for p0 in range(0, n - 1, 256):
             nv = min(256, n - 1 - p0)
             chunks.append((nv, next(m for m in (32, 64, 128, 256) if nv <= m)))
-        # weight passes: the qkv / gate-up GEMMs read a weight row once per min(M, 128) rows, wo / down once
-        # per min(M, 64) (engine.hip pf_bm); qkv + gate-up are ~2/3 of a Llama layer's weights
-        passes = sum((2.0 / 3.0) * (M // min(M, 128)) + (1.0 / 3.0) * (M // min(M, 64)) for _, M in chunks)
+        # weight passes: a GEMM workgroup reads its weight rows once per BM chunk rows (engine.hip
+        # StepRecorder::pg tilings); the workgroups of one row block share an XCD and run together, so HBM
+        # sees ~one pass per chunk and the rest are L2 hits (PMC: profiles/r3_prefill_pmc.txt)
+        D, Il, QD = cfg.hidden_size, cfg.intermediate_size, cfg.num_attention_heads * cfg.head_dim
+        KVD = cfg.num_key_value_heads * cfg.head_dim
+        role_w = {"qkv": D * (QD + 2 * KVD), "gu": 2 * D * Il, "out": D * QD + D * Il}
+        tot_w = float(sum(role_w.values()))
+
+        def bm(role, M):
+            if a.w_dtype == "i8":
+                return 32 if M == 32 else 64 if (role == "out" or role == "gu" or M == 64) else 128
+            return 32 if (M == 32 or role == "out") else 64 if M == 64 else 128
+        passes = sum(role_w[r] / tot_w * (M // bm(r, M)) for _, M in chunks for r in role_w)
         useful = 2.0 * params * (n - 1) * world  # whole-job flops of the projections (1 flop per MAC x 2)
         issued = 4.0 * params * sum(M for _, M in chunks) * world  # hi + lo MFMAs over the padded rows
         out["prefill"] = {"prompt_tokens": n, "positions_prefilled": n - 1,
                           "chunks": [{"rows": nv, "padded": M} for nv, M in chunks],
                           "seconds": round(tp, 5), "tokens_per_s": round((n - 1) / tp, 1),
-                          "weight_passes": round(passes, 2) if mfma else n - 1,
-                          "weight_bytes_streamed": round((passes if mfma else n - 1) * layer_bytes * world),
+                          "hbm_weight_passes": len(chunks) if mfma else n - 1,
+                          "l2_weight_passes": round(passes, 2) if mfma else n - 1,
                           "projection_tflops": round(useful / tp / 1e12, 2),
                           "mfma_issued_tflops": round(issued / tp / 1e12, 2) if mfma else None,
                           "mfma_peak_tflops": 2500.0,

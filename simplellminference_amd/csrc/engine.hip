@@ -790,31 +790,45 @@ struct StepRecorder {
     // GEMM just wrote. No LM head: the prompt's logits are not used (teacher forcing); the last prompt
     // position runs as an ordinary decode step. Phases as record_phase: 2l = qkv, attention, wo; 2l+1 =
     // gate/up, down; under tensor parallelism each ends with the all-reduce of the chunk's residual rows.
-    static int pf_bm(int M, bool out) { return std::min(M, out ? 64 : 128); }
-    template <class Epi, int BM>
-    static int pg_bm(sli_model* m, const void* W, int N, int K, const __half* hi, const __half* lo, const Epi& e,
-                     int M) {
+    template <class Epi, class Cfg>
+    static int pg_cfg(sli_model* m, const void* W, int N, int K, const __half* hi, const __half* lo, const Epi& e,
+                      int M) {
         if constexpr (std::is_same<WT, float>::value) {
             return fail(SLI_ERR_ARG, "prefill needs fp16 or int8 weights");
         } else {
             const PgIn<WT> in{(const WT*)W, hi, lo, N, K, M};
-            SLI_HIP((launch_pgemm<Epi, BM, WT>(in, e, m->pf.ps, m->stream)));
+            SLI_HIP((launch_pgemm<Epi, Cfg, WT>(in, e, m->pf.ps, m->stream)));
             return SLI_OK;
         }
     }
+    // The GEMM tiling (prefill.h PgCfg<BM, WR, S>) per weight type, projection role and chunk size: the
+    // fastest of the tools/pgemm_lab sweep (profiles/r3_pgemm_lab.txt) on the 7B shapes at a 256-row chunk.
+    // role 0: qkv, 1: gate/up, 2: wo / down (N = D: few row blocks, so small chunk blocks for a full grid)
     template <class Epi>
     static int pg(sli_model* m, const void* W, int N, int K, const __half* hi, const __half* lo, const Epi& e, int M,
-                  int BM) {
-        if (BM == 32) return pg_bm<Epi, 32>(m, W, N, K, hi, lo, e, M);
-        if (BM == 64) return pg_bm<Epi, 64>(m, W, N, K, hi, lo, e, M);
-        return pg_bm<Epi, 128>(m, W, N, K, hi, lo, e, M);
+                  int role) {
+        if constexpr (std::is_same<WT, int8_t>::value) {
+            if (M == 32) return pg_cfg<Epi, PgCfg<32, 2, 4>>(m, W, N, K, hi, lo, e, M);
+            if (role == 2) return pg_cfg<Epi, PgCfg<64, 2, 2>>(m, W, N, K, hi, lo, e, M);
+            if (role == 1 || M == 64) return pg_cfg<Epi, PgCfg<64, 4, 2>>(m, W, N, K, hi, lo, e, M);
+            return pg_cfg<Epi, PgCfg<128, 4, 2>>(m, W, N, K, hi, lo, e, M);
+        } else {
+            if (M == 32 || role == 2) return pg_cfg<Epi, PgCfg<32, 2, 4>>(m, W, N, K, hi, lo, e, M);
+            if (M == 64) return pg_cfg<Epi, PgCfg<64, 2, 3>>(m, W, N, K, hi, lo, e, M);
+            return pg_cfg<Epi, PgCfg<128, 2, 2>>(m, W, N, K, hi, lo, e, M);
+        }
     }
     template <class Epi>
     static int allow_pg(sli_model*) {
-        if constexpr (!std::is_same<WT, float>::value) {
-            SLI_HIP((pgemm_allow_lds<Epi, 32, WT>()));
-            SLI_HIP((pgemm_allow_lds<Epi, 64, WT>()));
-            SLI_HIP((pgemm_allow_lds<Epi, 128, WT>()));
+        if constexpr (std::is_same<WT, int8_t>::value) {
+            SLI_HIP((pgemm_allow_lds<Epi, PgCfg<32, 2, 4>, WT>()));
+            SLI_HIP((pgemm_allow_lds<Epi, PgCfg<64, 2, 2>, WT>()));
+            SLI_HIP((pgemm_allow_lds<Epi, PgCfg<64, 4, 2>, WT>()));
+            SLI_HIP((pgemm_allow_lds<Epi, PgCfg<128, 4, 2>, WT>()));
+        } else if constexpr (std::is_same<WT, __half>::value) {
+            SLI_HIP((pgemm_allow_lds<Epi, PgCfg<32, 2, 4>, WT>()));
+            SLI_HIP((pgemm_allow_lds<Epi, PgCfg<64, 2, 3>, WT>()));
+            SLI_HIP((pgemm_allow_lds<Epi, PgCfg<128, 2, 2>, WT>()));
         }
         return SLI_OK;
     }
@@ -843,22 +857,30 @@ struct StepRecorder {
         if (p % 2 == 0) {
             const size_t ls = (size_t)l * m->hkv * m->T * hd;
             PgEpiQKV<KT> eq{f.q, (KT*)m->kc + ls, (KT*)m->vc + ls, w.qkv_s, m->sin_t, m->cos_t, m->hq, m->hkv, hd, m->T};
-            SLI_TRY(pg(m, w.qkv, (m->hq + 2 * m->hkv) * hd, D, f.hhi, f.hlo, eq, M, pf_bm(M, false)));
+            SLI_TRY(pg(m, w.qkv, (m->hq + 2 * m->hkv) * hd, D, f.hhi, f.hlo, eq, M, 0));
             PfAttnArgs<KT> aa{f.q, (const KT*)m->kc + ls, (const KT*)m->vc + ls, f.hhi, f.hlo, m->hq, m->hkv, m->T,
                               1.0f / sqrtf((float)hd)};
-            const dim3 ag((M + kPaQB - 1) / kPaQB, m->hq);
-            if (hd == 128)
-                hipLaunchKernelGGL((pf_attn_kernel<KT, 128>), ag, dim3(256), 0, s, aa, f.ps);
-            else
-                hipLaunchKernelGGL((pf_attn_kernel<KT, 64>), ag, dim3(256), 0, s, aa, f.ps);
+            if constexpr (std::is_same<KT, __half>::value) {  // MFMA, 16 chunk rows per workgroup
+                const dim3 ag(M / 16, m->hq);
+                if (hd == 128)
+                    hipLaunchKernelGGL((pf_attn_mfma_kernel<128>), ag, dim3(256), 0, s, aa, f.ps);
+                else
+                    hipLaunchKernelGGL((pf_attn_mfma_kernel<64>), ag, dim3(256), 0, s, aa, f.ps);
+            } else {  // fp32 cache: fp32 VALU, 64 chunk rows per workgroup
+                const dim3 ag((M + kPaQB - 1) / kPaQB, m->hq);
+                if (hd == 128)
+                    hipLaunchKernelGGL((pf_attn_kernel<KT, 128>), ag, dim3(256), 0, s, aa, f.ps);
+                else
+                    hipLaunchKernelGGL((pf_attn_kernel<KT, 64>), ag, dim3(256), 0, s, aa, f.ps);
+            }
             SLI_HIP(hipGetLastError());
             er.rscale = w.wo_s;
-            return pg(m, w.wo, D, QD, f.hhi, f.hlo, er, M, pf_bm(M, true));
+            return pg(m, w.wo, D, QD, f.hhi, f.hlo, er, M, 2);
         }
         PgEpiSwiGLU eg{f.ahi, f.alo, w.gu_s, m->Il, m->c.act_mode};
-        SLI_TRY(pg(m, w.gu, 2 * m->Il, D, f.hhi, f.hlo, eg, M, pf_bm(M, false)));
+        SLI_TRY(pg(m, w.gu, 2 * m->Il, D, f.hhi, f.hlo, eg, M, 1));
         er.rscale = w.down_s;
-        return pg(m, w.down, D, m->Il, f.ahi, f.alo, er, M, pf_bm(M, true));
+        return pg(m, w.down, D, m->Il, f.ahi, f.alo, er, M, 2);
     }
     static int record_prefill(sli_model* m, int M) {
         for (int p = 0; p < 2 * m->L; ++p) {
@@ -1366,7 +1388,7 @@ static int get_state(sli_model* m, int seq, int32_t* pos, int32_t* token, int32_
 // the same tokens.
 static bool pf_supported(const sli_model* m) {
     return m->c.w_dtype != SLI_DT_F32 && m->B == 1 && (m->hd == 64 || m->hd == 128) && m->D % 64 == 0 &&
-           m->Il % 64 == 0 && (m->hq * m->hd) % 64 == 0;
+           m->D <= 8192 && m->Il % 64 == 0 && (m->hq * m->hd) % 64 == 0;
 }
 
 static int pf_bucket(int nv) {

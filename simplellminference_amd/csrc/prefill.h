@@ -24,9 +24,6 @@
 namespace sli {
 
 constexpr int kPfMaxChunk = 256;   // prompt positions per weight pass
-constexpr int kPgThreads = 256;    // 4 waves: 2 (row halves) x 2 (position halves)
-constexpr int kPgBN = 64;          // weight rows per workgroup
-constexpr int kPgStages = 3;       // LDS ring depth (k-blocks of 32)
 
 struct PfState {
     int32_t p0;  // position of chunk row 0
@@ -60,16 +57,26 @@ __global__ void __launch_bounds__(256) pf_embed_kernel(const PfState* __restrict
     for (int i = threadIdx.x; i < D; i += 256) x[(size_t)m * D + i] = to_f32(emb[(size_t)tok * D + i]) * s;
 }
 
-// one workgroup per chunk row: h = (x * 1/rms) * w (rms_kernel.cpp:12-22) or plain x (w == nullptr), as hi/lo
+// one workgroup per chunk row: h = (x * 1/rms) * w (rms_kernel.cpp:12-22) or plain x (w == nullptr), as hi/lo.
+// The row is held in registers (a float4 per thread and pass; D % 4 == 0, D <= 8192): one read of x, 8-byte
+// hi / lo stores.
 __global__ void __launch_bounds__(256) pf_norm_split_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                            __half* __restrict__ hi, __half* __restrict__ lo, int D,
                                                            float eps) {
+    constexpr int MAXV = 8;  // float4 per thread: D <= 8192
     const int m = blockIdx.x;
     const float* xr = x + (size_t)m * D;
+    const int n4 = D / 4;
+    float4 v[MAXV];
+    float ss = 0.0f;
+#pragma unroll
+    for (int j = 0; j < MAXV; ++j)
+        if (j * 256 + (int)threadIdx.x < n4) {
+            v[j] = reinterpret_cast<const float4*>(xr)[j * 256 + threadIdx.x];
+            ss += v[j].x * v[j].x + v[j].y * v[j].y + v[j].z * v[j].z + v[j].w * v[j].w;
+        }
     float inv = 1.0f;
     if (w) {
-        float ss = 0.0f;
-        for (int i = threadIdx.x; i < D; i += 256) ss += xr[i] * xr[i];
         ss = wave_sum(ss);
         __shared__ float red[4];
         if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
@@ -79,10 +86,17 @@ __global__ void __launch_bounds__(256) pf_norm_split_kernel(const float* __restr
         const float rms = sqrtf(tep + eps);  // :18
         inv = 1.0f / rms;                    // :19
     }
-    for (int i = threadIdx.x; i < D; i += 256) {
-        const float v = w ? (xr[i] * inv) * w[i] : xr[i];  // :20-22
-        pf_split(v, hi[(size_t)m * D + i], lo[(size_t)m * D + i]);
-    }
+#pragma unroll
+    for (int j = 0; j < MAXV; ++j)
+        if (j * 256 + (int)threadIdx.x < n4) {
+            const int i = (j * 256 + threadIdx.x) * 4;
+            const float f[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+            __half hh[4], hl[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) pf_split(w ? (f[e] * inv) * w[i + e] : f[e], hh[e], hl[e]);  // :20-22
+            *reinterpret_cast<uint2*>(hi + (size_t)m * D + i) = *reinterpret_cast<const uint2*>(hh);
+            *reinterpret_cast<uint2*>(lo + (size_t)m * D + i) = *reinterpret_cast<const uint2*>(hl);
+        }
 }
 
 // ---------------------------------------------------------------- 2. the GEMM
@@ -113,21 +127,45 @@ struct PgIn {
     int N, K, M;        // rows, depth, chunk rows (a multiple of BM)
 };
 
-// Stage geometry. A stage covers KBS k-blocks of 32: fp16 weights one (a weight image = 16 rows x 32 k),
-// int8 two (a weight image = 16 rows x 64 k int8 — the same 1 KiB). Images per stage: 4 weight row tiles,
-// then for each position tile and k-block the hi and the lo image.
+// Tiling: a workgroup of 2 WR waves owns BN = 32 WR weight rows x BM chunk rows; wave w holds the 2 x BM/32
+// accumulator tiles of rows 32 (w % WR) .. +32 and position half w / WR. A stage covers KS depth: 64 for fp16
+// weights, 128 for int8, so a weight row's slice is one whole 128-byte line (a chunk row's fp16 hi / lo slice
+// one or two lines). Each LDS-DMA wave-instruction moves 1 KiB of whole lines (8 rows x 128 B or 4 x 256 B;
+// fragment-shaped pieces of 16 rows x 64 B fetched every line twice and capped the ingest at ~29 GB/s per
+// CU, tools/pgemm_lab); the 16-byte chunks of a row are XOR-swizzled by the row so the fragment reads
+// (16 rows x 16 B per lane group) stay conflict-free. S stages in the LDS ring, S - 1 of them in flight.
 // Epilogue contract: row(t, i) = weight row of 16-row tile t's row i (i < 16, always valid); store(t, i0, m, v)
 // gets the fp32 sums of tile rows i0 .. i0+3 (i0 % 4 == 0) for chunk row m.
-template <int BM, typename WT>
-struct PgGeo {
-    static constexpr int KBS = sizeof(WT) == 1 ? 2 : 1;
-    static constexpr int PT = BM / 16;             // position tiles per workgroup
-    static constexpr int WPT = PT / 2;             // per wave
-    static constexpr int NDMA = 4 + 2 * PT * KBS;  // 1-KiB images per stage
-    static constexpr int DPW = NDMA / 4;           // per wave
-    static constexpr int STAGE = NDMA * 1024;
-    static_assert(WPT >= 1 && NDMA % 4 == 0, "BM");
+template <int BM_, int WR_, int S_>
+struct PgCfg {
+    static constexpr int BM = BM_, WR = WR_, S = S_;
 };
+
+template <class Cfg, typename WT>
+struct PgGeo {
+    static constexpr int BM = Cfg::BM, WR = Cfg::WR, S = Cfg::S;
+    static constexpr int WAVES = 2 * WR, THREADS = 64 * WAVES, BN = 32 * WR;
+    static constexpr int KS = sizeof(WT) == 1 ? 128 : 64;  // depth per stage
+    static constexpr int KBS = KS / 32;                    // MFMA k-blocks per stage
+    static constexpr int A_ROW = KS * (int)sizeof(WT);     // 128 B
+    static constexpr int B_ROW = KS * 2;                   // 128 or 256 B
+    static constexpr int A_IMG = 16 * A_ROW, B_IMG = 16 * B_ROW;
+    static constexpr int PT = BM / 16;  // position tiles per workgroup
+    static constexpr int WPT = PT / 2;  // per wave
+    static constexpr int NA = 2 * WR;   // weight row tiles
+    static constexpr int A_BYTES = NA * A_IMG;
+    static constexpr int STAGE = A_BYTES + 2 * PT * B_IMG;
+    static constexpr int NDMA = STAGE / 1024;  // wave-instructions per stage
+    static constexpr int DPW = NDMA / WAVES;   // per wave
+    static constexpr size_t LDS = (size_t)S * STAGE;
+    static_assert(A_ROW == 128 && WPT >= 1 && NDMA % WAVES == 0, "tiling");
+    static_assert(S >= 2 && (S - 1) * DPW <= 63, "ring depth (vmcnt counts 63 loads)");
+    static_assert(LDS <= 160 * 1024, "LDS");
+};
+
+// 16-byte chunk swizzle of an image row (conflict-free fragment reads): rows of 128 B pair up in one 256-B
+// bank span, so the chunk index is XORed with row / 2; rows of 256 B with the row
+__device__ __forceinline__ int pg_swz(int row, int row_bytes) { return row_bytes == 128 ? (row >> 1) & 7 : row & 15; }
 
 // 8 int8 weights -> 8 fp16 (exact): fp16 bits 0x6400 | (b ^ 0x80) = 1024 + b + 128, minus 1152
 __device__ __forceinline__ u32x4 pg_i8_to_f16(uint2 w) {
@@ -146,48 +184,68 @@ __device__ __forceinline__ u32x4 pg_i8_to_f16(uint2 w) {
     return r;
 }
 
-template <class Epi, int BM, typename WT>
-__global__ void __launch_bounds__(kPgThreads) pgemm_kernel(PgIn<WT> in, Epi epi, const PfState* __restrict__ ps) {
-    using Geo = PgGeo<BM, WT>;
-    constexpr int KBS = Geo::KBS;
+// wait until at most `later` stages of DPW images each are still in flight (later: 0 .. 6)
+template <int DPW>
+__device__ __forceinline__ void pg_wait_stages(int later) {
+    switch (later) {
+        case 0: pf_wait_vm<0>(); break;
+        case 1: pf_wait_vm<1 * DPW>(); break;
+        case 2: pf_wait_vm<(2 * DPW > 63 ? 63 : 2 * DPW)>(); break;
+        case 3: pf_wait_vm<(3 * DPW > 63 ? 63 : 3 * DPW)>(); break;
+        case 4: pf_wait_vm<(4 * DPW > 63 ? 63 : 4 * DPW)>(); break;
+        case 5: pf_wait_vm<(5 * DPW > 63 ? 63 : 5 * DPW)>(); break;
+        default: pf_wait_vm<(6 * DPW > 63 ? 63 : 6 * DPW)>(); break;
+    }
+}
+
+template <class Epi, class Cfg, typename WT>
+__global__ void __launch_bounds__(128 * Cfg::WR) pgemm_kernel(PgIn<WT> in, Epi epi, const PfState* __restrict__ ps) {
+    using Geo = PgGeo<Cfg, WT>;
+    constexpr int KBS = Geo::KBS, BM = Geo::BM, WR = Geo::WR, S = Geo::S;
     extern __shared__ __attribute__((aligned(1024))) char pg_smem[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int wr = wave & 1, wp = wave >> 1;  // row half, position half
+    const int wr = wave % WR, wp = wave / WR;  // row pair, position half
     const int PB = in.M / BM;
     // workgroups that share a row block run on one XCD (blocks b and b + 8 share one under round-robin
     // placement; speed only): the second read of the weight rows hits that XCD's L2
     const int bid = blockIdx.x, xcd = bid & 7, slot = bid >> 3;
     const int rb = (slot / PB) * 8 + xcd, pb = slot - (slot / PB) * PB;
-    const int nrb = (in.N + kPgBN - 1) / kPgBN;
+    const int nrb = (in.N + Geo::BN - 1) / Geo::BN;
     if (rb >= nrb) return;  // (uniform) padding of the grid to a multiple of 8 row blocks
-    const int ns = in.K / (32 * KBS);  // stages
+    const int ns = in.K / Geo::KS;  // stages
+    const int nt = in.N >> 4;       // row tiles
     const unsigned ring = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)pg_smem;
 
-    // this wave's DMA images: image d in [wave*DPW, (wave+1)*DPW). Lane l of an image: fragment row / column
-    // l & 15, k group l >> 4 (8 fp16 or 16 int8 elements).
-    const int kg = lane >> 4, c16 = lane & 15;
+    // this wave's DMA instructions d in [wave*DPW, (wave+1)*DPW): stage bytes [1024 d, 1024 (d + 1)). Lane i
+    // lands at byte 16 i of it: image row i / cpr, physical chunk i % cpr (cpr = 16-B chunks per image row),
+    // so it loads the row's logical chunk (i % cpr) ^ swizzle(row).
     const char* src[Geo::DPW];
     int adv[Geo::DPW];  // bytes per stage
 #pragma unroll
     for (int j = 0; j < Geo::DPW; ++j) {
-        const int d = wave * Geo::DPW + j;
-        if (d < 4) {
-            const int t = rb * 4 + d;
-            const int row = epi.row(min(t, (in.N >> 4) - 1), c16);
-            src[j] = reinterpret_cast<const char*>(in.W) + (size_t)row * in.K * sizeof(WT) + kg * 16;
-            adv[j] = 64;
+        const int off = (wave * Geo::DPW + j) * 1024;
+        if (off < Geo::A_BYTES) {
+            const int t = rb * Geo::NA + off / Geo::A_IMG;
+            const int r = (off % Geo::A_IMG) / Geo::A_ROW + lane / 8;
+            const int c = (lane % 8) ^ pg_swz(r, Geo::A_ROW);
+            const int row = epi.row(min(t, nt - 1), r);
+            src[j] = reinterpret_cast<const char*>(in.W) + (size_t)row * in.K * sizeof(WT) + c * 16;
+            adv[j] = Geo::A_ROW;
         } else {
-            const int e = d - 4, r = e >> 1;
-            const int pt = r / KBS, kb = r - pt * KBS;
-            const __half* B = (e & 1) ? in.Blo : in.Bhi;
-            const int m = pb * BM + pt * 16 + c16;
-            src[j] = reinterpret_cast<const char*>(B) + ((size_t)m * in.K + kb * 32 + kg * 8) * 2;
-            adv[j] = 64 * KBS;
+            constexpr int cpr = Geo::B_ROW / 16;
+            const int o2 = off - Geo::A_BYTES;
+            const int u = o2 / Geo::B_IMG, pt = u >> 1;
+            const int r = (o2 % Geo::B_IMG) / Geo::B_ROW + lane / cpr;
+            const int c = (lane % cpr) ^ pg_swz(r, Geo::B_ROW);
+            const __half* B = (u & 1) ? in.Blo : in.Bhi;
+            const int m = pb * BM + pt * 16 + r;
+            src[j] = reinterpret_cast<const char*>(B) + (size_t)m * in.K * 2 + c * 16;
+            adv[j] = Geo::B_ROW;
         }
     }
     auto issue = [&](int s) {
-        const unsigned dst = ring + (unsigned)((s % kPgStages) * Geo::STAGE);
+        const unsigned dst = ring + (unsigned)((s % S) * Geo::STAGE);
 #pragma unroll
         for (int j = 0; j < Geo::DPW; ++j)
             pf_dma(src[j] + (size_t)s * adv[j], dst + (unsigned)((wave * Geo::DPW + j) * 1024));
@@ -199,35 +257,35 @@ __global__ void __launch_bounds__(kPgThreads) pgemm_kernel(PgIn<WT> in, Epi epi,
 #pragma unroll
         for (int b = 0; b < Geo::WPT; ++b) acc[a][b] = pf_float4{0.0f, 0.0f, 0.0f, 0.0f};
 
-    issue(0);
-    if (ns > 1) issue(1);
+    // fragment read offsets: lane l reads row / column r = l & 15, k group kg = l >> 4 of each 32-k block
+    const int kg = lane >> 4, r16 = lane & 15;
+    const int sa = pg_swz(r16, Geo::A_ROW), sb = pg_swz(r16, Geo::B_ROW);
+    for (int s = 0; s < S - 1 && s < ns; ++s) issue(s);
     for (int s = 0; s < ns; ++s) {
-        if (s + 1 < ns)
-            pf_wait_vm<Geo::DPW>();  // this wave's images of stage s landed (s + 1 may stay in flight)
-        else
-            pf_wait_vm<0>();
-        __builtin_amdgcn_s_barrier();  // every wave's images of s landed; every wave is done with s - 1
-        if (s + 2 < ns) issue(s + 2);  // into the buffer of s - 1
-        const char* st = pg_smem + (size_t)(s % kPgStages) * Geo::STAGE;
+        // this wave's pieces of stage s landed (stages s + 1 .. s + S - 2 may stay in flight)
+        pg_wait_stages<Geo::DPW>(min(S - 2, ns - 1 - s));
+        __builtin_amdgcn_s_barrier();  // every wave's pieces of s landed; every wave is done with s - 1
+        if (s + S - 1 < ns) issue(s + S - 1);  // into the buffer of s - 1
+        const char* st = pg_smem + (size_t)(s % S) * Geo::STAGE;
 #pragma unroll
         for (int kb = 0; kb < KBS; ++kb) {
             u32x4 af[2], bh[Geo::WPT], bl[Geo::WPT];
 #pragma unroll
             for (int a = 0; a < 2; ++a) {
-                const char* img = st + (wr * 2 + a) * 1024;
-                if constexpr (KBS == 1) {
-                    af[a] = reinterpret_cast<const u32x4*>(img)[lane];
-                } else {  // k 32 kb + 8 (l >> 4) .. +8 of row l & 15: 16-k group 2 kb + (l >> 5), half (l >> 4) & 1
-                    const int off = ((2 * kb + (lane >> 5)) * 16 + c16) * 16 + 8 * ((lane >> 4) & 1);
+                const char* img = st + (wr * 2 + a) * Geo::A_IMG + r16 * Geo::A_ROW;
+                if constexpr (sizeof(WT) == 2) {
+                    af[a] = *reinterpret_cast<const u32x4*>(img + ((4 * kb + kg) ^ sa) * 16);
+                } else {  // k 32 kb + 8 kg .. +8: chunk 2 kb + kg / 2, half kg % 2
+                    const int off = ((2 * kb + (kg >> 1)) ^ sa) * 16 + 8 * (kg & 1);
                     af[a] = pg_i8_to_f16(*reinterpret_cast<const uint2*>(img + off));
                 }
             }
 #pragma unroll
             for (int b = 0; b < Geo::WPT; ++b) {
                 const int pt = wp * Geo::WPT + b;
-                const u32x4* bi = reinterpret_cast<const u32x4*>(st + (4 + 2 * (pt * KBS + kb)) * 1024) + lane;
-                bh[b] = bi[0];
-                bl[b] = bi[64];
+                const char* img = st + Geo::A_BYTES + (2 * pt) * Geo::B_IMG + r16 * Geo::B_ROW + ((4 * kb + kg) ^ sb) * 16;
+                bh[b] = *reinterpret_cast<const u32x4*>(img);
+                bl[b] = *reinterpret_cast<const u32x4*>(img + Geo::B_IMG);
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
@@ -243,11 +301,11 @@ __global__ void __launch_bounds__(kPgThreads) pgemm_kernel(PgIn<WT> in, Epi epi,
     const int i0 = 4 * (lane >> 4);
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
-        const int t = rb * 4 + wr * 2 + a;
-        if (t >= (in.N >> 4)) continue;
+        const int t = rb * Geo::NA + wr * 2 + a;
+        if (t >= nt) continue;
 #pragma unroll
         for (int b = 0; b < Geo::WPT; ++b) {
-            const int m = pb * BM + (wp * Geo::WPT + b) * 16 + c16;
+            const int m = pb * BM + (wp * Geo::WPT + b) * 16 + r16;
             const float v[4] = {acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]};
             epi.store(t, i0, m, v, ps);
         }
@@ -272,36 +330,49 @@ struct PgEpiQKV {  // model.cpp:52-67: q (fp32 [M][hq*hd]), rotated k / v rows o
         return uh * hd + d + ((i & 2) ? half : 0);
     }
     __device__ void store(int t, int i0, int m, const float* v, const PfState* ps) const {
+        // units u, u + 1 (u even): d, d + 1 of one head (hd / 2 is even), so every store is a pair
         const int nv = ps->nv, pos = ps->p0 + m;
         const int half = hd >> 1;
+        const int u = t * 8 + (i0 >> 2) * 2;
+        const int uh = u / half, d = u - uh * half;
+        float a0[2] = {v[0], v[1]}, a1[2] = {v[2], v[3]};  // first / second element of the pairs of u, u + 1
+        if (rscale) {
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const int u = t * 8 + (i0 >> 2) * 2 + e;
-            const int uh = u / half, d = u - uh * half;
-            float a0 = v[e], a1 = v[2 + e];
-            if (rscale) {
-                a0 *= rscale[uh * hd + d];
-                a1 *= rscale[uh * hd + d + half];
+            for (int e = 0; e < 2; ++e) {
+                a0[e] *= rscale[uh * hd + d + e];
+                a1[e] *= rscale[uh * hd + d + e + half];
             }
-            if (uh < hq + hkv) {  // rope_kernel.cpp:30-38
-                const int pp = min(pos, T - 1);
-                const float fci = sin_t[pp * half + d], fcr = cos_t[pp * half + d];
-                const float r0 = a0 * fcr - a1 * fci;
-                const float r1 = a1 * fcr + a0 * fci;
-                if (uh < hq) {
-                    float* qr = q + (size_t)m * hq * hd + (size_t)uh * hd;
-                    qr[d] = r0;
-                    qr[d + half] = r1;
-                } else if (m < nv && pos < T) {
-                    KT* kr = kc + ((size_t)(uh - hq) * T + pos) * hd;
-                    kr[d] = from_f32<KT>(r0);
-                    kr[d + half] = from_f32<KT>(r1);
-                }
+        }
+        if (uh < hq + hkv) {  // rope_kernel.cpp:30-38
+            const int pp = min(pos, T - 1);
+            float r0[2], r1[2];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const float fci = sin_t[pp * half + d + e], fcr = cos_t[pp * half + d + e];
+                r0[e] = a0[e] * fcr - a1[e] * fci;
+                r1[e] = a1[e] * fcr + a0[e] * fci;
+            }
+            if (uh < hq) {
+                float* qr = q + (size_t)m * hq * hd + (size_t)uh * hd;
+                *reinterpret_cast<float2*>(qr + d) = make_float2(r0[0], r0[1]);
+                *reinterpret_cast<float2*>(qr + d + half) = make_float2(r1[0], r1[1]);
             } else if (m < nv && pos < T) {
-                KT* vr = vc + ((size_t)(uh - hq - hkv) * T + pos) * hd;
-                vr[d] = from_f32<KT>(a0);
-                vr[d + half] = from_f32<KT>(a1);
+                KT* kr = kc + ((size_t)(uh - hq) * T + pos) * hd;
+                store2(kr + d, r0);
+                store2(kr + d + half, r1);
             }
+        } else if (m < nv && pos < T) {
+            KT* vr = vc + ((size_t)(uh - hq - hkv) * T + pos) * hd;
+            store2(vr + d, a0);
+            store2(vr + d + half, a1);
+        }
+    }
+    __device__ static void store2(KT* p, const float* f) {
+        if constexpr (sizeof(KT) == 2) {
+            __half h[2] = {__float2half_rn(f[0]), __float2half_rn(f[1])};
+            *reinterpret_cast<unsigned*>(p) = *reinterpret_cast<const unsigned*>(h);
+        } else {
+            *reinterpret_cast<float2*>(p) = make_float2(f[0], f[1]);
         }
     }
 };
@@ -313,18 +384,21 @@ struct PgEpiSwiGLU {  // model.cpp:99-115: act = sigmoid(g) * u (or SiLU), store
     int inter, silu;
     __device__ int row(int t, int i) const { return t * 8 + (i >> 2) * 2 + (i & 1) + ((i & 2) ? inter : 0); }
     __device__ void store(int t, int i0, int m, const float* v, const PfState*) const {
+        const int u = t * 8 + (i0 >> 2) * 2;  // units u, u + 1: one 4-byte hi and lo store each
+        __half hh[2], hl[2];
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
-            const int u = t * 8 + (i0 >> 2) * 2 + e;
             float g = v[e], up = v[2 + e];
             if (rscale) {
-                g *= rscale[u];
-                up *= rscale[inter + u];
+                g *= rscale[u + e];
+                up *= rscale[inter + u + e];
             }
             float sg = 1.0f / (1.0f + expf(-g));  // swiglu_kernel.cpp:12
             if (silu) sg = g * sg;
-            pf_split(sg * up, ahi[(size_t)m * inter + u], alo[(size_t)m * inter + u]);  // :13
+            pf_split(sg * up, hh[e], hl[e]);  // :13
         }
+        *reinterpret_cast<unsigned*>(ahi + (size_t)m * inter + u) = *reinterpret_cast<const unsigned*>(hh);
+        *reinterpret_cast<unsigned*>(alo + (size_t)m * inter + u) = *reinterpret_cast<const unsigned*>(hl);
     }
 };
 
@@ -335,36 +409,35 @@ struct PgEpiResid {  // y[m][row] = resid[m][row] + sum * row scale (matmul_kern
     int nrows, ld;
     __device__ int row(int t, int i) const { return min(t * 16 + i, nrows - 1); }
     __device__ void store(int t, int i0, int m, const float* v, const PfState*) const {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int row = t * 16 + i0 + r;
-            if (row >= nrows) continue;
-            const size_t i = (size_t)m * ld + row;
-            const float p = rscale ? v[r] * rscale[row] : v[r];
-            y[i] = resid ? resid[i] + p : p;
+        const int row = t * 16 + i0;  // rows row .. row + 3 (nrows % 16 == 0: the host's check)
+        const size_t i = (size_t)m * ld + row;
+        float4 p = make_float4(v[0], v[1], v[2], v[3]);
+        if (rscale) {
+            const float4 sc = *reinterpret_cast<const float4*>(rscale + row);
+            p = make_float4(p.x * sc.x, p.y * sc.y, p.z * sc.z, p.w * sc.w);
         }
+        if (resid) {
+            const float4 r = *reinterpret_cast<const float4*>(resid + i);
+            p = make_float4(r.x + p.x, r.y + p.y, r.z + p.z, r.w + p.w);
+        }
+        *reinterpret_cast<float4*>(y + i) = p;
     }
 };
 
-template <int BM, typename WT>
-constexpr size_t pgemm_lds_bytes() {
-    return (size_t)kPgStages * PgGeo<BM, WT>::STAGE;
-}
-
-template <class Epi, int BM, typename WT>
+template <class Epi, class Cfg, typename WT>
 hipError_t launch_pgemm(const PgIn<WT>& in, const Epi& epi, const PfState* ps, hipStream_t s) {
-    const int nrb = (in.N + kPgBN - 1) / kPgBN;
+    using Geo = PgGeo<Cfg, WT>;
+    const int nrb = (in.N + Geo::BN - 1) / Geo::BN;
     const int nrb8 = (nrb + 7) / 8 * 8;
-    const dim3 grid(nrb8 * (in.M / BM));
-    constexpr size_t lds = pgemm_lds_bytes<BM, WT>();
-    hipLaunchKernelGGL((pgemm_kernel<Epi, BM, WT>), grid, dim3(kPgThreads), lds, s, in, epi, ps);
+    const dim3 grid(nrb8 * (in.M / Geo::BM));
+    hipLaunchKernelGGL((pgemm_kernel<Epi, Cfg, WT>), grid, dim3(Geo::THREADS), Geo::LDS, s, in, epi, ps);
     return hipGetLastError();
 }
 
-template <class Epi, int BM, typename WT>
+template <class Epi, class Cfg, typename WT>
 hipError_t pgemm_allow_lds() {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&pgemm_kernel<Epi, BM, WT>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)pgemm_lds_bytes<BM, WT>());
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&pgemm_kernel<Epi, Cfg, WT>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)PgGeo<Cfg, WT>::LDS);
 }
 
 // ---------------------------------------------------------------- 3. block-causal attention
@@ -448,6 +521,190 @@ __global__ void __launch_bounds__(256) pf_attn_kernel(PfAttnArgs<KT> a, const Pf
     for (int e = 0; e < QD; ++e) {
         const size_t idx = (size_t)mi * a.hq * HD + (size_t)h * HD + c * QD + e;
         pf_split(o[e] / l, a.ohi[idx], a.olo[idx]);
+    }
+}
+
+// ---- 3b. block-causal attention on MFMA (fp16 cache). A workgroup = 16 chunk rows (queries) of one head;
+// its 4 waves split the key range into 32-key tiles (wave w takes tiles w, w + 4, ...) and merge their
+// (max, sum, o) through LDS at the end. Per tile a wave:
+//   - LDS-DMAs K and V rows t0 .. t0+31 (16 x 1 KiB pieces) into its own images, 16-B chunks XOR-swizzled;
+//   - Sᵀ = K Qᵀ: C[key][query] on v_mfma_f32_16x16x32_f16, A = K rows (exact fp16), B = Qᵀ as hi + lo fp16
+//     (two MFMAs into one accumulator);
+//   - online softmax per query (a lane's 8 keys, then the 4 lane groups of a query by xor 16 / 32);
+//   - Oᵀ += Vᵀ Pᵀ: B = Pᵀ straight from the Sᵀ accumulators (lane l holds query l & 15, keys
+//     {4g .. 4g+3, 16+4g .. 16+4g+3}, g = l >> 4 — the k order of the B operand), P as hi + lo; A = Vᵀ by
+//     two ds_read_b64_tr_b16 per 16-d tile, whose 4-row blocks are exactly those keys.
+// mha_kernel.cpp:36-77 per query: s_t = (q . k_t) * scale, softmax over t <= position, o = sum p_t v_t.
+template <int HD>
+struct PaGeo {
+    static constexpr int ROWB = HD * 2;          // bytes per image row
+    static constexpr int IMG = 32 * ROWB;        // one 32-key image
+    static constexpr int WAVE = 2 * IMG;         // K + V
+    static constexpr int PIECES = WAVE / 1024;   // DMA instructions per tile
+    static constexpr int CPR = ROWB / 16;        // 16-B chunks per row
+};
+__device__ __forceinline__ int pa_swz_k(int r, int rowb) { return rowb == 256 ? r & 15 : (r >> 1) & 7; }
+__device__ __forceinline__ int pa_swz_v(int r, int rowb) { return rowb == 256 ? (r & 7) << 1 : ((r >> 1) & 3) << 1; }
+
+__device__ __forceinline__ uint2 pa_tr_read(unsigned lds_addr) {
+    uint2 v;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(lds_addr) : "memory");
+    return v;
+}
+
+template <int HD>
+__global__ void __launch_bounds__(256) pf_attn_mfma_kernel(PfAttnArgs<__half> a, const PfState* __restrict__ ps) {
+    using G = PaGeo<HD>;
+    constexpr int ND = HD / 32, NT = HD / 16;  // 32-d blocks (S), 16-d tiles (O)
+    __shared__ __attribute__((aligned(1024))) char sm[4 * G::WAVE];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int g = lane >> 4, i16 = lane & 15;
+    const int h = blockIdx.y, kvh = h / (a.hq / a.hkv);
+    const int p0 = ps->p0;
+    const int mq = blockIdx.x * 16 + i16;  // this lane's query (chunk row)
+    const int pos = p0 + mq;
+    const int last = min(p0 + blockIdx.x * 16 + 15, a.T - 1);  // the group's last query position
+    const int ntiles = last / 32 + 1;
+    const size_t qs = (size_t)a.hq * HD;
+    // Qᵀ as the B operand: lane l = query l & 15, d = 32 db + 8 g .. +8, fp32 -> hi + lo
+    u32x4 qh[ND], ql[ND];
+#pragma unroll
+    for (int db = 0; db < ND; ++db) {
+        const float4* qp = reinterpret_cast<const float4*>(a.q + (size_t)mq * qs + (size_t)h * HD + db * 32 + g * 8);
+        const float4 v0 = qp[0], v1 = qp[1];
+        const float f[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        __half hh[8], hl[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) pf_split(f[e], hh[e], hl[e]);
+        qh[db] = *reinterpret_cast<const u32x4*>(hh);
+        ql[db] = *reinterpret_cast<const u32x4*>(hl);
+    }
+    pf_float4 o[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) o[t] = pf_float4{0.0f, 0.0f, 0.0f, 0.0f};
+    float mx = -INFINITY, l = 0.0f;
+    char* kimg = sm + wave * G::WAVE;
+    char* vimg = kimg + G::IMG;
+    const unsigned kbase = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)kimg;
+    const unsigned vbase = kbase + G::IMG;
+    const __half* kc = a.kc + (size_t)kvh * a.T * HD;
+    const __half* vc = a.vc + (size_t)kvh * a.T * HD;
+    for (int tt = wave; tt < ntiles; tt += 4) {
+        const int t0 = tt * 32;
+        // K pieces 0 .. P/2-1, V pieces P/2 .. P-1; lane i of a piece: row (piece rows) + i / CPR, physical
+        // chunk i % CPR <- logical chunk (i % CPR) ^ swizzle(row)
+#pragma unroll
+        for (int j = 0; j < G::PIECES; ++j) {
+            const bool isv = j >= G::PIECES / 2;
+            const int jj = isv ? j - G::PIECES / 2 : j;
+            const int r = jj * (1024 / G::ROWB) + lane / G::CPR;
+            const int c = (lane % G::CPR) ^ (isv ? pa_swz_v(r, G::ROWB) : pa_swz_k(r, G::ROWB));
+            const __half* src = (isv ? vc : kc) + (size_t)min(t0 + r, a.T - 1) * HD + c * 8;
+            pf_dma(src, (isv ? vbase : kbase) + (unsigned)(jj * 1024));
+        }
+        pf_wait_vm<0>();
+        // Sᵀ[key][query] for keys t0 + 16 kt + (0..15)
+        pf_float4 sacc[2];
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+            sacc[kt] = pf_float4{0.0f, 0.0f, 0.0f, 0.0f};
+            const int r = kt * 16 + i16;
+            const char* krow = kimg + r * G::ROWB;
+#pragma unroll
+            for (int db = 0; db < ND; ++db) {
+                const u32x4 kf = *reinterpret_cast<const u32x4*>(krow + ((4 * db + g) ^ pa_swz_k(r, G::ROWB)) * 16);
+                sacc[kt] = pf_mfma(kf, qh[db], sacc[kt]);
+                sacc[kt] = pf_mfma(kf, ql[db], sacc[kt]);
+            }
+        }
+        // lane holds keys t0 + 16 kt + 4 g + r of query mq
+        float sv[8];
+        float cmax = -INFINITY;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int key = t0 + kt * 16 + 4 * g + r;
+                const float v = key <= pos ? sacc[kt][r] * a.scale : -INFINITY;
+                sv[kt * 4 + r] = v;
+                cmax = fmaxf(cmax, v);
+            }
+        cmax = fmaxf(cmax, __shfl_xor(cmax, 16));
+        cmax = fmaxf(cmax, __shfl_xor(cmax, 32));
+        const float mn = fmaxf(mx, cmax);
+        const float corr = mn == -INFINITY ? 1.0f : expf(mx - mn);
+        float pv[8], psum = 0.0f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            pv[e] = sv[e] == -INFINITY ? 0.0f : expf(sv[e] - mn);
+            psum += pv[e];
+        }
+        psum += __shfl_xor(psum, 16);
+        psum += __shfl_xor(psum, 32);
+        l = l * corr + psum;
+        mx = mn;
+        __half ph[8], pl[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) pf_split(pv[e], ph[e], pl[e]);
+        const u32x4 pfh = *reinterpret_cast<const u32x4*>(ph);
+        const u32x4 pfl = *reinterpret_cast<const u32x4*>(pl);
+        // Vᵀ 16-d tile dt: lane 16 g + 4 q + p addresses row (4 g + q) [+16], d 16 dt + 4 p .. +3
+        const int q4 = (lane & 15) >> 2, p4 = lane & 3;
+        const int r1 = 4 * g + q4, r2 = 16 + 4 * g + q4;
+        const unsigned a1 = vbase + r1 * G::ROWB + 8 * (p4 & 1), a2 = vbase + r2 * G::ROWB + 8 * (p4 & 1);
+        const int s1 = pa_swz_v(r1, G::ROWB), s2 = pa_swz_v(r2, G::ROWB);
+        uint2 x1[NT], x2[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int c = 2 * t + (p4 >> 1);
+            x1[t] = pa_tr_read(a1 + ((c ^ s1) * 16));
+            x2[t] = pa_tr_read(a2 + ((c ^ s2) * 16));
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            o[t] *= corr;
+            const u32x4 vf = u32x4{x1[t].x, x1[t].y, x2[t].x, x2[t].y};
+            o[t] = pf_mfma(vf, pfh, o[t]);
+            o[t] = pf_mfma(vf, pfl, o[t]);
+        }
+    }
+    // merge the 4 key splits: wave w publishes (mx, l, o) and merges 16-d tiles t = w, w + 4, ...
+    __syncthreads();
+    float* fo = reinterpret_cast<float*>(sm);                         // [wave][NT][64 lanes][4]
+    float* fm = fo + 4 * NT * 64 * 4;                                 // [wave][64]
+    float* fl = fm + 4 * 64;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+        *reinterpret_cast<pf_float4*>(fo + ((wave * NT + t) * 64 + lane) * 4) = o[t];
+    fm[wave * 64 + lane] = mx;
+    fl[wave * 64 + lane] = l;
+    __syncthreads();
+    float m4[4], w4[4], M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        m4[w] = fm[w * 64 + lane];
+        M = fmaxf(M, m4[w]);
+    }
+    float L = 0.0f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        w4[w] = m4[w] == -INFINITY ? 0.0f : expf(m4[w] - M);
+        L += fl[w * 64 + lane] * w4[w];
+    }
+    const float inv = 1.0f / L;
+    for (int t = wave; t < NT; t += 4) {
+        pf_float4 acc = pf_float4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int w = 0; w < 4; ++w) acc += *reinterpret_cast<const pf_float4*>(fo + ((w * NT + t) * 64 + lane) * 4) * w4[w];
+        // lane holds d = 16 t + 4 g + r of query mq
+        const size_t idx = (size_t)mq * qs + (size_t)h * HD + t * 16 + 4 * g;
+        __half hh[4], hl[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pf_split(acc[r] * inv, hh[r], hl[r]);
+        *reinterpret_cast<uint2*>(a.ohi + idx) = *reinterpret_cast<const uint2*>(hh);
+        *reinterpret_cast<uint2*>(a.olo + idx) = *reinterpret_cast<const uint2*>(hl);
     }
 }
 
