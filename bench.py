@@ -274,13 +274,18 @@ def main():
               "final_pos_ok": all(x["pos"] == a.ctx - 1 for x in gst) and not any(x["error"] for x in gst)}
 
     traffic, traffic_family = None, {}
+    tkey = f"{a.preset}/{a.w_dtype}/tp{world}" + (f"/b{B}" if B > 1 else "")
+    traffic_source = {"file": os.path.relpath(a.traffic_json, ROOT), "key": tkey, "family": dom,
+                      "field": "per_family_hbm_bytes_per_launch", "found": False,
+                      "note": "rocprofv3 --pmc FETCH_SIZE pass (tools/pmc_traffic.sh), KiB x 1024 x 2 (gfx950 correction); "
+                              "a committed builder pass, not measured in this run"}
     if os.path.exists(a.traffic_json):
         try:
             tj = json.load(open(a.traffic_json))
-            key = f"{a.preset}/{a.w_dtype}/tp{world}" + (f"/b{B}" if B > 1 else "")
-            if key in tj:
-                traffic_family = tj[key].get("per_family_hbm_bytes_per_launch", {})
+            if tkey in tj:
+                traffic_family = tj[tkey].get("per_family_hbm_bytes_per_launch", {})
                 traffic = traffic_family.get(dom)
+                traffic_source["found"] = traffic is not None
         except (OSError, ValueError, KeyError):
             traffic = None
 
@@ -309,7 +314,7 @@ def main():
         "tp_allreduce": allreduce,
         "roofline": {"bound": "hbm", "kernel": f"{dom}: {FAMILY_KERNELS[B > 1][dom]}",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_source,
                      "avg_launch_us": round(d["avg_us"], 3), "algorithmic_bytes_per_launch": round(d["bytes_per_launch"]),
                      "stream_floor_us": round(sfl[dom], 3) if dom in sfl else None,
                      "stream_floor_gbs": (round(d["bytes_per_launch"] / (sfl[dom] * 1e-6) / 1e9, 1)

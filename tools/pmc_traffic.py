@@ -4,7 +4,10 @@ FETCH_SIZE is in KiB and, on gfx950, reads exactly half the bytes of a wide coal
 (cdna_hip_programming.md section 7; MI355X_MICROARCH.md HBM), so traffic = 2 * FETCH_SIZE * 1024. Only
 the decode step's own GEMV dispatches are counted: the weight-placement and KV-fill kernels at model
 build are skipped by name.
-    python tools/pmc_traffic.py <counter_collection.csv> <algorithmic bytes per launch> <out.json> <key>
+    python tools/pmc_traffic.py <counter_collection.csv> <dominant family's algorithmic bytes per launch> <out.json>
+                                <key> [<dominant family>]
+Top-level fields: the mean over EVERY weight-streaming launch of the step (all families together), then the
+dominant family's own algorithmic bytes; per-family HBM bytes per launch are in per_family_hbm_bytes_per_launch.
 """
 import csv
 import json
@@ -12,6 +15,7 @@ import sys
 from collections import defaultdict
 
 path, alg, out, key = sys.argv[1], float(sys.argv[2]), sys.argv[3], sys.argv[4]
+dom = sys.argv[5] if len(sys.argv) > 5 else None  # the bench line's dominant family (whose bytes alg are)
 per = defaultdict(list)
 for r in csv.DictReader(open(path)):
     if r.get("Counter_Name") != "FETCH_SIZE":
@@ -31,13 +35,14 @@ try:
 except (OSError, ValueError):
     pass
 res[key] = {
-    "hbm_bytes_per_launch": round(2 * kb * 1024),
-    "fetch_size_kib_per_launch_raw": round(kb, 1),
+    "all_weight_kernels_mean_hbm_bytes_per_launch": round(2 * kb * 1024),
+    "all_weight_kernels_mean_fetch_size_kib_raw": round(kb, 1),
     "correction": ("x2: gfx950 FETCH_SIZE counts half the bytes of a coalesced 16-B/lane stream"
                    + ("" if "bgemm" not in "".join(per) else "; bgemm's 16-row x 64-B fragment loads are "
                       "not calibrated against that rule")),
-    "algorithmic_bytes_per_launch": round(alg),
-    "gemv_dispatches": len(gemv),
+    "dominant_family": dom,
+    "dominant_family_algorithmic_bytes_per_launch": round(alg),
+    "weight_kernel_dispatches": len(gemv),
     "per_kernel_mean_kib_raw": {k.split("(")[0][:90]: round(sum(v) / len(v), 1) for k, v in per.items()
                                 if weight_kernel(k)},
 }
@@ -65,5 +70,7 @@ for k, vs in per.items():
     if f:
         fam[f] += vs
 res[key]["per_family_hbm_bytes_per_launch"] = {f: round(2 * 1024 * sum(v) / len(v)) for f, v in fam.items()}
+if dom in res[key]["per_family_hbm_bytes_per_launch"]:
+    res[key]["dominant_family_hbm_over_algorithmic"] = round(res[key]["per_family_hbm_bytes_per_launch"][dom] / alg, 4)
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res[key], indent=1))
