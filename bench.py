@@ -65,8 +65,9 @@ def parse():
     ap.add_argument("--exec", default="launches", choices=["launches", "persistent"],
                     help="launches: one graph of fused launches (default, fastest measured); persistent: the whole "
                          "step as one launch with grid barriers (batch 1, TP 1; DESIGN.md §4)")
-    ap.add_argument("--tp-allreduce", default="auto", choices=["auto", "rccl", "oneshot"],
-                    help="TP all-reduce: auto = the one-shot xGMI kernel if a validation step against RCCL agrees on "
+    ap.add_argument("--tp-allreduce", default="auto", choices=["auto", "rccl", "oneshot", "fused"],
+                    help="TP all-reduce: auto = the one-shot exchange fused into the wo / down launches (batch 1; "
+                         "the separate one-shot kernel at batch > 1) if a validation step against RCCL agrees on "
                          "every rank, else RCCL")
     ap.add_argument("--prefill-tokens", type=int, default=512,
                     help="after the decode timing: prefill a prompt of this many tokens (0: skip; batch 1 only)")
@@ -140,7 +141,7 @@ def _oneshot_opened(model, dist, torch, mode) -> bool:
         progress(f"one-shot buffers unavailable on this rank: {e}")
     flag = torch.tensor([0 if err else 1], dtype=torch.int32)
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-    if flag.item() == 0 and mode == "oneshot":  # forced one-shot: EVERY rank stops (none waits on RCCL alone)
+    if flag.item() == 0 and mode in ("oneshot", "fused"):  # forced one-shot: EVERY rank stops (none waits on RCCL alone)
         raise SystemExit(f"one-shot buffers could not be mapped on every rank ({err or 'another rank failed'})")
     return flag.item() == 1
 
@@ -195,27 +196,28 @@ def main():
     allreduce = "none"
     if dist_on:
         allreduce = "rccl"
+        os_mode = a.tp_allreduce if a.tp_allreduce in ("oneshot", "fused") else ("fused" if B == 1 else "oneshot")
         if os.environ.get("SLI_DEBUG_NOCOMM") and a.tp_allreduce != "rccl":
             # debug (several ranks on one GPU, no RCCL communicator): the one-shot kernels are the only exchange
             from simplellminference_amd import tp
             tp.open_oneshot(model)
-            model.set_allreduce("oneshot")
-            allreduce = "oneshot (SLI_DEBUG_NOCOMM: not validated against rccl)"
+            model.set_allreduce(os_mode)
+            allreduce = f"{os_mode} (SLI_DEBUG_NOCOMM: not validated against rccl)"
         elif a.tp_allreduce != "rccl" and not _oneshot_opened(model, dist, torch, a.tp_allreduce):
             allreduce = "rccl (one-shot buffers could not be mapped on every rank)"
         elif a.tp_allreduce != "rccl":
             import numpy as np
             model.step()  # RCCL reference step (idempotent: position ctx-1 is recomputed)
             ref = model.logits()[0].copy()
-            model.set_allreduce("oneshot")
+            model.set_allreduce(os_mode)
             model.step()
             got = model.logits()[0]
             ok = bool(model.state()["error"] == 0 and np.isfinite(got).all() and np.abs(got - ref).max() <= 1e-3)
             flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
             dist.all_reduce(flag, op=dist.ReduceOp.MIN)
             if flag.item() == 1:
-                allreduce = "oneshot (validated against rccl on every rank)"
-            elif a.tp_allreduce == "oneshot":
+                allreduce = f"{os_mode} (validated against rccl on every rank)"
+            elif a.tp_allreduce in ("oneshot", "fused"):
                 raise SystemExit("one-shot all-reduce disagrees with RCCL")
             else:
                 model.set_allreduce("rccl")

@@ -151,8 +151,11 @@ int sli_tp_vocab(const sli_model_config* cfg, int32_t* vocab_lo, int32_t* vocab_
  * handles over any host transport, each opens all of them with sli_model_comm_open (handles [nranks][
  * sli_model_comm_handle_bytes()] in rank order) and switches with sli_model_set_allreduce. Each call
  * pushes the rank's partial to every rank, raises a flag per rank, waits (bounded) for all flags and
- * sums in rank order, so every rank holds bit-identical x; the argmax keys use the same exchange. */
-enum { SLI_ALLREDUCE_RCCL = 0, SLI_ALLREDUCE_ONESHOT = 1 };
+ * sums in rank order, so every rank holds bit-identical x; the argmax keys use the same exchange.
+ * SLI_ALLREDUCE_FUSED (batch 1): the same exchange inside the wo / down GEMV launches — their epilogues
+ * push the finished rows into the peers' slots and the launch's last workgroup waits and sums (no
+ * separate all-reduce launch). */
+enum { SLI_ALLREDUCE_RCCL = 0, SLI_ALLREDUCE_ONESHOT = 1, SLI_ALLREDUCE_FUSED = 2 };
 int sli_model_comm_handle_bytes(void);
 int sli_model_comm_handle(sli_model* m, void* out, int32_t n);
 int sli_model_comm_open(sli_model* m, const void* handles, int32_t nranks);

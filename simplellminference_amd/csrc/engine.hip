@@ -103,8 +103,10 @@ struct sli_model {
     char* os_peer[sli::kOsMaxRanks] = {};    // every rank's buffer mapped here (own included)
     bool os_open = false;
     bool os_dead = false;                    // a one-shot wait timed out: set_allreduce(ONESHOT) is refused
-    unsigned* os_epoch = nullptr;            // one-shot call counter
+    unsigned* os_epoch = nullptr;            // one-shot call counter; os_epoch[1..9]: fused-launch arrivals
     int os_nmax = 0;
+    bool os_loopback = false;                // debug: SLI_DEBUG_OS_LOOPBACK (oneshot.h OneShotArgs::loopback)
+    char** os_peer_tab = nullptr;            // device copy of os_peer (oneshot.h EpiPush::peer_tab)
     size_t os_bytes = 0;
     // SLI_EXEC_PERSISTENT (persist.h): the whole step as one launch
     int exec = SLI_EXEC_LAUNCHES;
@@ -530,6 +532,14 @@ struct StepRecorder {
         EpiStore<1> e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, w.wo_s, 1.0f, m->D};
         const AttnMergeIn am{m->part, &m->st->pos, attn_max_splits(m), attn_wg_positions(m->c.kv_dtype, m->hd), m->hd};
         constexpr int UW = 2;  // int8 too (tools/gemv_lab i8: R1U2 7.5 us vs R1U1 7.95 on the 4096x4096 shape)
+        if (fused_ar(m)) {
+            const EpiPush<1> ep = push_epi(m, w.wo_s);
+            if (am.max_splits > 8)
+                SLI_HIP((launch_gemv_merge<WT, 1, UW, NT, EpiPush<1>, 16>((const WT*)w.wo, in, ep, am, m->D, m->stream)));
+            else
+                SLI_HIP((launch_gemv_merge<WT, 1, UW, NT, EpiPush<1>>((const WT*)w.wo, in, ep, am, m->D, m->stream)));
+            return SLI_OK;
+        }
         // contexts past 8 splits (ctx > 2048 at hd 128 fp16): the 16-split input batch (ctx 4096 wo: 13.6 us
         // with splits 8..15 read one by one during the merge)
         if (am.max_splits > 8)
@@ -553,6 +563,14 @@ struct StepRecorder {
         const LayerW& w = m->layers[l];
         const bool tp = m->partial;
         GemvIn in{m->act, nullptr, 0.0f, m->Il};
+        if (fused_ar(m)) {
+            const EpiPush<1> ep = push_epi(m, w.down_s);
+            if constexpr (std::is_same<WT, int8_t>::value)
+                SLI_HIP((launch_gemv<WT, 1, 4, NT>((const WT*)w.down, in, ep, m->D, m->stream)));
+            else
+                SLI_HIP((launch_gemv_u<WT, 1, 6, NT>((const WT*)w.down, in, ep, m->D, m->stream)));
+            return SLI_OK;
+        }
         EpiStore<1> e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, w.down_s, 1.0f, m->D};
         if constexpr (std::is_same<WT, int8_t>::value)  // tools/gemv_lab i8: R1U4 11.66 us vs R1U3 11.74
             SLI_HIP((launch_gemv<WT, 1, 4, NT>((const WT*)w.down, in, e, m->D, m->stream)));
@@ -572,6 +590,22 @@ struct StepRecorder {
         SLI_HIP((launch_gemv_u<WT, 2, 4, NT>(w, in, e, (m->v_n + 1) / 2, m->stream)));
         return SLI_OK;
     }
+    // the residual all-reduce inside the wo / down launch (oneshot.h EpiPush), batch 1
+    static bool fused_ar(const sli_model* m) { return m->partial && m->ar_mode == SLI_ALLREDUCE_FUSED; }
+    static EpiPush<1> push_epi(sli_model* m, const float* rscale) {
+        OneShotArgs a{};
+        for (int r = 0; r < m->c.tp_size; ++r) a.peers[r] = m->os_peer[r];
+        a.rank = m->c.tp_rank;
+        a.nranks = m->c.tp_size;
+        a.n = m->D;
+        a.nmax = m->os_nmax;
+        a.src = nullptr;
+        a.dst = m->x;
+        a.epoch = m->os_epoch;
+        a.st = m->st;
+        a.loopback = m->os_loopback;
+        return EpiPush<1>{m->c.tp_rank == 0 ? m->x : nullptr, rscale, 1.0f, m->D, a, m->os_epoch + 1, m->os_peer_tab};
+    }
     static int oneshot(sli_model* m, const void* src, void* dst, int n, bool max_u64) {
         OneShotArgs a{};
         for (int r = 0; r < m->c.tp_size; ++r) a.peers[r] = m->os_peer[r];
@@ -583,6 +617,7 @@ struct StepRecorder {
         a.dst = (float*)dst;
         a.epoch = m->os_epoch;
         a.st = m->st;
+        a.loopback = m->os_loopback;
         if (max_u64)
             hipLaunchKernelGGL(oneshot_kernel<1>, dim3(1), dim3(1024), 0, m->stream, a);
         else
@@ -592,6 +627,7 @@ struct StepRecorder {
     }
     static int allreduce_x(sli_model* m) {
         const size_t n = (size_t)m->B * m->D;
+        if (fused_ar(m)) return SLI_OK;  // done inside the wo / down launch
         if (m->ar_mode == SLI_ALLREDUCE_ONESHOT) return oneshot(m, m->xpart, m->x, (int)n, false);
         if (m->collectives)
             SLI_NCCL(ncclAllReduce(m->xpart, m->x, n, ncclFloat32, ncclSum, m->comm, m->stream));
@@ -736,7 +772,8 @@ struct StepRecorder {
             SLI_TRY(record_phase(m, p));
             SLI_TRY(allreduce_x(m));
         }
-        if (m->ar_mode == SLI_ALLREDUCE_ONESHOT) {  // the argmax keys through the same one-shot exchange
+        if (m->ar_mode == SLI_ALLREDUCE_ONESHOT || m->ar_mode == SLI_ALLREDUCE_FUSED) {  // the argmax keys through
+                                                                                          // the one-shot exchange
             SLI_TRY(record_head(m, true));
             void* k = m->B > 1 ? (void*)m->bkeys : (void*)&m->st->key;
             SLI_TRY(oneshot(m, k, k, 2 * m->B, true));
@@ -1758,8 +1795,9 @@ int sli_model_comm_handle(sli_model* m, void* out, int32_t n) {
         m->os_bytes = 256 + sizeof(float) * 2 * (size_t)kOsMaxRanks * m->os_nmax;
         SLI_HIP(hipExtMallocWithFlags((void**)&m->os_buf, m->os_bytes, hipDeviceMallocUncached));
         SLI_HIP(hipMemset(m->os_buf, 0, m->os_bytes));
-        SLI_TRY(model_alloc(m, (void**)&m->os_epoch, sizeof(unsigned)));
-        SLI_HIP(hipMemset(m->os_epoch, 0, sizeof(unsigned)));
+        SLI_TRY(model_alloc(m, (void**)&m->os_epoch, 16 * sizeof(unsigned)));
+        SLI_HIP(hipMemset(m->os_epoch, 0, 16 * sizeof(unsigned)));
+        SLI_TRY(model_alloc(m, (void**)&m->os_peer_tab, sizeof(char*) * kOsMaxRanks));
     }
     hipIpcMemHandle_t h;
     SLI_HIP(hipIpcGetMemHandle(&h, m->os_buf));
@@ -1786,13 +1824,27 @@ int sli_model_comm_open(sli_model* m, const void* handles, int32_t nranks) {
         SLI_HIP(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
         m->os_peer[r] = (char*)p;
     }
+    SLI_HIP(hipMemcpy(m->os_peer_tab, m->os_peer, sizeof(char*) * kOsMaxRanks, hipMemcpyHostToDevice));
     m->os_open = true;
     return SLI_OK;
 }
 
 int sli_model_set_allreduce(sli_model* m, int32_t mode) {
     SLI_CHECK(m, SLI_ERR_ARG, "null model");
-    SLI_CHECK(mode == SLI_ALLREDUCE_RCCL || mode == SLI_ALLREDUCE_ONESHOT, SLI_ERR_ARG, "unknown all-reduce mode");
+    if (mode != SLI_ALLREDUCE_RCCL && !m->os_open && getenv("SLI_DEBUG_OS_LOOPBACK") && m->partial && !m->collectives) {
+        // debug timing on one GPU without peers (with SLI_DEBUG_NOCOMM): every peer slot is this rank's own
+        // buffer and the rank raises every flag itself; the sums are not a model
+        char h[256];
+        SLI_TRY(sli_model_comm_handle(m, h, (int32_t)sizeof(h)));
+        for (int r = 0; r < m->c.tp_size; ++r) m->os_peer[r] = m->os_buf;
+        SLI_HIP(hipMemcpy(m->os_peer_tab, m->os_peer, sizeof(char*) * kOsMaxRanks, hipMemcpyHostToDevice));
+        m->os_open = true;
+        m->os_loopback = true;
+    }
+    SLI_CHECK(mode == SLI_ALLREDUCE_RCCL || mode == SLI_ALLREDUCE_ONESHOT || mode == SLI_ALLREDUCE_FUSED, SLI_ERR_ARG,
+              "unknown all-reduce mode");
+    SLI_CHECK(mode != SLI_ALLREDUCE_FUSED || m->B == 1, SLI_ERR_STATE,
+              "the fused all-reduce rides the batch-1 GEMV epilogues (batch > 1: oneshot or rccl)");
     SLI_CHECK(mode == SLI_ALLREDUCE_RCCL || m->os_open, SLI_ERR_STATE, "one-shot all-reduce: open the peers first");
     SLI_CHECK(mode == SLI_ALLREDUCE_RCCL || !m->os_dead, SLI_ERR_STATE,
               "one-shot all-reduce: a wait timed out earlier, the ranks' epochs may disagree");

@@ -34,6 +34,8 @@ struct OneShotArgs {
     float* dst;                // the reduced result
     unsigned* epoch;           // this rank's call counter (plain device memory)
     DevState* st;              // error reporting
+    int loopback = 0;          // debug (one process, SLI_DEBUG_OS_LOOPBACK): every peer is this rank's own buffer
+                               // and the rank raises every rank's flag (timing of the exchange without peers)
 };
 
 __device__ __forceinline__ unsigned* os_flag(char* buf, int par, int r) {
@@ -41,6 +43,76 @@ __device__ __forceinline__ unsigned* os_flag(char* buf, int par, int r) {
 }
 __device__ __forceinline__ float* os_data(char* buf, int par, int r, int nmax) {
     return reinterpret_cast<float*>(buf + 256) + ((size_t)par * kOsMaxRanks + r) * nmax;
+}
+
+// Flags, bounded wait and the rank-order reduction of epoch e, by threads [0, nthr) of ONE workgroup
+// whose pushes (and, in the fused form, every pushing workgroup's) have drained: raise flag[par][rank] on
+// every rank (system-scope release), wait until this rank's flags[par][*] all read e (system-scope
+// acquire, bounded), reduce data[par][0 .. N-1] in rank order into dst, advance the epoch.
+// peers: the ranks' buffers, indexed by a runtime rank — the kernel-argument array, or a device-memory table
+// (a runtime index into a struct held in a per-thread copy, as the GEMV epilogues are, would put the whole
+// struct in scratch memory)
+template <int OP>
+__device__ __forceinline__ void os_finish(const OneShotArgs& a, char* const* peers, unsigned e, int* abort_lds) {
+    const int par = (int)(e & 1u);
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    if (tid < a.nranks)
+        __hip_atomic_store(os_flag(peers[tid], par, a.loopback ? tid : a.rank), e, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    if (tid == 0) *abort_lds = 0;
+    __syncthreads();
+    if (tid < a.nranks) {
+        unsigned* f = os_flag(peers[a.rank], par, tid);
+        for (unsigned spins = 0; __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != e; ++spins) {
+            if (spins >= kOsSpinLimit) {
+                __hip_atomic_fetch_or(&a.st->error, kOsErrTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                *abort_lds = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __syncthreads();
+    if (*abort_lds) {
+        // stay in step with the peers that did not time out (they advance the epoch), and make the stale
+        // result loud: NaN instead of the previous call's values (DevState::error already records it)
+        if constexpr (OP == 0)
+            for (int i = tid; i < a.n; i += nthr) a.dst[i] = __builtin_nanf("");
+        if (tid == 0) *a.epoch = e;
+        return;
+    }
+    char* mine = peers[a.rank];
+    if constexpr (OP == 0) {
+        const int n4 = a.n >> 2;  // fp32 sums: n is a multiple of 4 (B * D)
+        for (int i = tid; i < n4; i += nthr) {
+            float4 v[kOsMaxRanks];  // every rank's slot in flight at once (one round trip), then summed
+#pragma unroll
+            for (int r = 0; r < kOsMaxRanks; ++r)
+                v[r] = reinterpret_cast<const float4*>(os_data(mine, par, min(r, a.nranks - 1), a.nmax))[i];
+            float4 acc = v[0];
+#pragma unroll
+            for (int r = 1; r < kOsMaxRanks; ++r) {  // rank order: every rank adds identically
+                if (r < a.nranks) {
+                    acc.x += v[r].x;
+                    acc.y += v[r].y;
+                    acc.z += v[r].z;
+                    acc.w += v[r].w;
+                }
+            }
+            reinterpret_cast<float4*>(a.dst)[i] = acc;
+        }
+    } else {
+        const int nk = a.n >> 1;
+        for (int i = tid; i < nk; i += nthr) {
+            unsigned long long b = 0;
+            for (int r = 0; r < a.nranks; ++r) {
+                const unsigned long long k = reinterpret_cast<const unsigned long long*>(os_data(mine, par, r, a.nmax))[i];
+                b = k > b ? k : b;
+            }
+            reinterpret_cast<unsigned long long*>(a.dst)[i] = b;
+        }
+    }
+    if (tid == 0) *a.epoch = e;
 }
 
 // OP 0: sum of fp32; OP 1: max of u64 (argmax keys, two floats per element)
@@ -64,57 +136,85 @@ __global__ void __launch_bounds__(1024) oneshot_kernel(OneShotArgs a) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid < a.nranks)
-        __hip_atomic_store(os_flag(a.peers[tid], par, a.rank), e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    // wait for every rank's contribution in my own buffer
     __shared__ int abort;
-    if (tid == 0) abort = 0;
-    __syncthreads();
-    if (tid < a.nranks) {
-        unsigned* f = os_flag(a.peers[a.rank], par, tid);
-        for (unsigned spins = 0; __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != e; ++spins) {
-            if (spins >= kOsSpinLimit) {
-                __hip_atomic_fetch_or(&a.st->error, kOsErrTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                abort = 1;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    __syncthreads();
-    if (abort) {
-        // stay in step with the peers that did not time out (they advance the epoch), and make the stale
-        // result loud: NaN instead of the previous call's values (DevState::error already records it)
-        if constexpr (OP == 0)
-            for (int i = tid; i < a.n; i += blockDim.x) a.dst[i] = __builtin_nanf("");
-        if (tid == 0) *a.epoch = e;
-        return;
-    }
-    char* mine = a.peers[a.rank];
-    if constexpr (OP == 0) {
-        for (int i = tid; i < n4; i += blockDim.x) {
-            float4 acc = reinterpret_cast<const float4*>(os_data(mine, par, 0, a.nmax))[i];
-            for (int r = 1; r < a.nranks; ++r) {  // rank order: every rank adds identically
-                const float4 v = reinterpret_cast<const float4*>(os_data(mine, par, r, a.nmax))[i];
-                acc.x += v.x;
-                acc.y += v.y;
-                acc.z += v.z;
-                acc.w += v.w;
-            }
-            reinterpret_cast<float4*>(a.dst)[i] = acc;
-        }
-    } else {
-        const int nk = a.n >> 1;
-        for (int i = tid; i < nk; i += blockDim.x) {
-            unsigned long long b = 0;
-            for (int r = 0; r < a.nranks; ++r) {
-                const unsigned long long k = reinterpret_cast<const unsigned long long*>(os_data(mine, par, r, a.nmax))[i];
-                b = k > b ? k : b;
-            }
-            reinterpret_cast<unsigned long long*>(a.dst)[i] = b;
-        }
-    }
-    if (tid == 0) *a.epoch = e;
+    os_finish<OP>(a, a.peers, e, &abort);
 }
+
+// The residual all-reduce fused into the row-parallel GEMV that produces the partial (wo, down; batch 1):
+// the epilogue pushes each finished row sum (rank 0: plus the residual) straight into slot [rank] of every
+// rank's comm buffer instead of a local partial; every workgroup drains its pushes and counts its arrival,
+// and the last workgroup to arrive runs os_finish (flags, bounded wait, rank-order sum into x, epoch). The
+// separate oneshot launch and its kernel boundary disappear; the next launch reads x as usual. Only one
+// workgroup per rank ever waits, so ranks that share a device cannot starve each other of CUs.
+// Epilogue contract: gemv.h (units / rows / prefetch_a / prefetch_b / store / finish).
+template <int R>
+struct EpiPush {
+    const float* resid;  // rank 0: the residual stream x; other ranks nullptr
+    const float* rscale;
+    float scale;
+    int nrows;
+    OneShotArgs os;      // dst = x, n = nrows (batch 1)
+    unsigned* arrive;    // [9] arrival counters (8 shards + top), zero between launches (last arrivers reset)
+    char* const* peer_tab;  // device copy of os.peers (the last arriver's runtime-indexed flags and slots)
+    unsigned e = 0;
+    int pre_u = -1;
+    float pre_r[R] = {}, pre_s[R] = {};
+    __device__ int units() const { return (nrows + R - 1) / R; }
+    __device__ void rows(int u, int* r) const {
+#pragma unroll
+        for (int i = 0; i < R; ++i) r[i] = min(u * R + i, nrows - 1);
+    }
+    __device__ void prefetch_a(int u) {
+        e = *os.epoch + 1;  // written by the previous all-reduce's last arriver (an earlier launch)
+        pre_u = u;
+        const float* rp = resid ? resid : rscale ? rscale : os.dst;
+        const float* sp = rscale ? rscale : os.dst;
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const int row = min(u * R + i, nrows - 1);
+            pre_r[i] = rp[row];
+            pre_s[i] = sp[row];
+        }
+    }
+    __device__ void prefetch_b(int) {}
+    __device__ void store(int u, const int*, const float* v) const {
+        const bool pre = u == pre_u;
+        const int par = (int)(e & 1u);
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const int row = u * R + i;
+            if (row < nrows) {
+                float a = rscale ? v[i] * (pre ? pre_s[i] : rscale[row]) : v[i];
+                a = a * scale;
+                if (resid) a = (pre ? pre_r[i] : resid[row]) + a;  // add_kernel.cpp:5-14, once (rank 0)
+#pragma unroll
+                for (int p = 0; p < kOsMaxRanks; ++p)
+                    if (p < os.nranks) os_data(os.peers[p], par, os.rank, os.nmax)[row] = a;
+            }
+        }
+    }
+    __device__ void finish(float* smem) const {
+        int* sh = reinterpret_cast<int*>(smem) + 40;  // [0]: last arriver, [1]: abort (gemv LDS head)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every pushing wave drains before the arrival
+        __syncthreads();
+        if (threadIdx.x == 0) {  // two-level arrival: a shard per blockIdx % 8 (an XCD under round-robin
+                                 // placement: speed only), then the shards' last arrivers on arrive[8]
+            const unsigned g = gridDim.x, sd = blockIdx.x & 7u;
+            const unsigned nsh = g < 8u ? g : 8u, cnt = (g - sd + 7u) >> 3;
+            int last = 0;
+            if (__hip_atomic_fetch_add(arrive + sd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == cnt - 1u) {
+                __hip_atomic_store(arrive + sd, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (__hip_atomic_fetch_add(arrive + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsh - 1u) {
+                    __hip_atomic_store(arrive + 8, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    last = 1;
+                }
+            }
+            sh[0] = last;
+        }
+        __syncthreads();
+        if (!sh[0]) return;  // uniform
+        os_finish<0>(os, peer_tab, e, sh + 1);
+    }
+};
 
 }  // namespace sli

@@ -186,8 +186,9 @@ class LlamaModel:
         return self
 
     def set_allreduce(self, mode: str) -> "LlamaModel":
-        """"rccl" (ncclAllReduce in the step graph) or "oneshot" (oneshot.h, after comm_open)."""
-        call("sli_model_set_allreduce", self._h, {"rccl": 0, "oneshot": 1}[mode])
+        """"rccl" (ncclAllReduce in the step graph), "oneshot" (oneshot.h, after comm_open) or "fused" (the
+        one-shot exchange inside the wo / down GEMV launches, batch 1; oneshot.h EpiPush)."""
+        call("sli_model_set_allreduce", self._h, {"rccl": 0, "oneshot": 1, "fused": 2}[mode])
         return self
 
     # ------------------------------------------------------------------ model.cpp:40-140

@@ -130,7 +130,7 @@ def test_tp_rank_of_c2_shapes_steps_nocomm(gpu, monkeypatch, w, world):
     m.close()
 
 
-def _oneshot_rank(rank, world, port, name, batch, q):
+def _oneshot_rank(rank, world, port, name, batch, q, mode="oneshot"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0",
                       SLI_DEBUG_NOCOMM="1")  # no RCCL communicator: the one-shot kernels are the only exchange
     import torch
@@ -144,7 +144,7 @@ def _oneshot_rank(rank, world, port, name, batch, q):
         m = LlamaModel(config=preset(name), w_dtype="f16", kv_dtype="f16", tp_rank=rank, tp_size=world,
                        device=dev, seed=0, batch=batch).init()
         tp.open_oneshot(m)
-        m.set_allreduce("oneshot")
+        m.set_allreduce(mode)
         dist.barrier()
         if batch == 1:
             toks, logits = m.predict(PROMPT, 16, want_logits=True)
@@ -162,11 +162,14 @@ def _oneshot_rank(rank, world, port, name, batch, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,batch", [("tiny", 1), ("tiny-gqa", 1), ("tiny-gqa", 2)])
-def test_oneshot_allreduce_two_processes(gpu, name, batch):
+@pytest.mark.parametrize("name,batch,mode", [("tiny", 1, "oneshot"), ("tiny-gqa", 1, "oneshot"), ("tiny-gqa", 2, "oneshot"),
+                                             ("tiny", 1, "fused"), ("tiny-gqa", 1, "fused"), ("tiny-h8", 1, "fused")])
+def test_oneshot_allreduce_two_processes(gpu, name, batch, mode):
     """The one-shot all-reduce (oneshot.h) between two rank PROCESSES through IPC-mapped uncached buffers
     (both on device 0 here; on the 8-GPU node each on its own GPU, over xGMI): greedy tokens identical to
-    the TP = 1 engine, logits within 1e-3, no device error (the bounded waits never gave up)."""
+    the TP = 1 engine, logits within 1e-3, no device error (the bounded waits never gave up). mode "fused":
+    the exchange runs inside the wo / down GEMV launches (EpiPush: rows pushed from the epilogue, the
+    launch's last workgroup waits and sums)."""
     from simplellminference_amd.model import LlamaModel, preset
     ref = LlamaModel(config=preset(name), w_dtype="f16", kv_dtype="f16", seed=0, batch=batch).init()
     if batch == 1:
@@ -177,7 +180,7 @@ def test_oneshot_allreduce_two_processes(gpu, name, batch):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_oneshot_rank, args=(r, 2, port, name, batch, q)) for r in range(2)]
+    procs = [ctx.Process(target=_oneshot_rank, args=(r, 2, port, name, batch, q, mode)) for r in range(2)]
     for p in procs:
         p.start()
     status, toks, logits, err = q.get(timeout=300)

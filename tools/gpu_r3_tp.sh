@@ -1,0 +1,12 @@
+#!/bin/bash
+# round 3: TP fused all-reduce tests + per-rank step timing (loopback), then the prefill MFMA counter pass
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_tp.py -x -v -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/tp_tests.log 2>&1 || { echo TP TESTS FAILED; tail -40 gpurun_out/tp_tests.log; exit 1; }
+grep -E "passed|failed|skipped" gpurun_out/tp_tests.log | tail -3
+timeout -k 10 300 python3 tools/tp_rank_time.py 1 2 4 8 > gpurun_out/tp_rank_time.txt 2>&1 || { cat gpurun_out/tp_rank_time.txt; exit 1; }
+TP_AR=oneshot timeout -k 10 300 python3 tools/tp_rank_time.py 2 4 8 >> gpurun_out/tp_rank_time.txt 2>&1 || { cat gpurun_out/tp_rank_time.txt; exit 1; }
+TP_AR=fused timeout -k 10 300 python3 tools/tp_rank_time.py 2 4 8 >> gpurun_out/tp_rank_time.txt 2>&1 || { cat gpurun_out/tp_rank_time.txt; exit 1; }
+cat gpurun_out/tp_rank_time.txt
+./tools/pmc_mfma.sh r3 llama2-7b/f16/tp1/prefill512 --prefill-tokens 512 --prefill-reps 1 || exit 1
+cat gpurun_out/pmc/r3_mfma.json

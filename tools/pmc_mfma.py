@@ -25,6 +25,13 @@ for r in csv.DictReader(open(path)):
 
 
 def family(k):
+    if "pgemm_kernel" in k:  # the prompt prefill's chunk GEMMs (prefill.h)
+        for tag, fam in (("PgEpiQKV", "prefill_qkv"), ("PgEpiSwiGLU", "prefill_gate_up"), ("PgEpiResid", "prefill_wo+down")):
+            if tag in k:
+                return fam
+        return "prefill_other"
+    if "pf_attn_mfma_kernel" in k:
+        return "prefill_attention"
     if "bgemm_kernel" not in k:
         return None
     for tag, fam in (("BgEpiQKV", "qkv"), ("BgEpiSwiGLU", "gate_up"), ("BgEpiLogits", "lm_head"),

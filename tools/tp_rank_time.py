@@ -2,6 +2,8 @@
 (SLI_DEBUG_NOCOMM: the rank's kernels at their real shapes, no RCCL all-reduces; values are not a model).
 Estimates the compute part of config C2 (Llama-2-7B at TP N); the collectives come on top.
     python tools/tp_rank_time.py [N ...]            (TP_EXEC=persistent: the one-launch step instead)
+TP_AR=oneshot|fused: the rank's all-reduces included, in loopback (SLI_DEBUG_OS_LOOPBACK: the exchange kernels
+run against the rank's own comm buffer, every flag raised locally — everything but the xGMI hop).
 """
 import os
 import sys
@@ -22,6 +24,10 @@ for world in [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]:
             m.set_exec(os.environ["TP_EXEC"])
         except Exception as e:  # noqa: BLE001 - report and go on with the launch graph
             print(f"tp{world}: {os.environ['TP_EXEC']} refused ({e})", flush=True)
+    ar = os.environ.get("TP_AR")
+    if ar and world > 1:
+        os.environ["SLI_DEBUG_OS_LOOPBACK"] = "1"
+        m.set_allreduce(ar)
     m.set_state(1234, 2047, advance=False)
     for _ in range(10):
         m.step()
@@ -32,6 +38,8 @@ for world in [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]:
         m.step()
     m.sync()
     ms = 1e3 * (time.perf_counter() - t0) / n
-    print(f"tp{world} rank {world - 1} [{m.exec_mode()}]: {ms:.3f} ms/step compute (no all-reduces)", flush=True)
+    what = f"all-reduces {ar} (loopback)" if ar and world > 1 else "no all-reduces"
+    print(f"tp{world} rank {world - 1} [{m.exec_mode()}]: {ms:.3f} ms/step compute ({what}); device error "
+          f"{m.state()['error']}", flush=True)
     m.close()
     m.close()
