@@ -60,6 +60,8 @@ def lib():
                                      ctypes.c_float]
         L.orc_model_create.argtypes = [ctypes.c_void_p]
         L.orc_model_create.restype = ctypes.c_void_p
+        L.orc_model_create_lazy.argtypes = [ctypes.c_void_p]
+        L.orc_model_create_lazy.restype = ctypes.c_void_p
         L.orc_model_free.argtypes = [ctypes.c_void_p]
         L.orc_model_init_synthetic.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int]
         L.orc_model_weight.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
@@ -213,11 +215,13 @@ class _CConfig(ctypes.Structure):
 class Model:
     """LlamaModel restatement (model.cpp:40-187) with synthetic weights (sli_synth.h)."""
 
-    def __init__(self, cfg: Config, seed: int = 0, wmode: int = W_F32, kv_f16: bool = False):
+    def __init__(self, cfg: Config, seed: int = 0, wmode: int = W_F32, kv_f16: bool = False, lazy: bool = False):
+        """lazy: hold one layer of weights and regenerate each layer inside forward (full-size models such as
+        the 32-layer Llama-2-7B step; weight() then serves only the embedding and norms)."""
         self.cfg = cfg
         c = _CConfig(cfg.vocab, cfg.dim, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, cfg.ffn, cfg.n_layers,
                      cfg.max_len, cfg.eps, cfg.theta)
-        self._h = lib().orc_model_create(ctypes.byref(c))
+        self._h = (lib().orc_model_create_lazy if lazy else lib().orc_model_create)(ctypes.byref(c))
         lib().orc_model_init_synthetic(self._h, seed, wmode)
         lib().orc_model_set_kv_f16(self._h, 1 if kv_f16 else 0)
 

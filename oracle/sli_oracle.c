@@ -6,10 +6,12 @@
 #include "sli_oracle.h"
 
 #include <math.h>
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <unistd.h>
 
 #include "../include/sli_synth.h"
 
@@ -229,7 +231,64 @@ struct orc_model {
     float *x, *h, *q, *score, *attn, *o, *x1, *u, *g, *a, *f;
     float *sin_c, *cos_c;
     double t_embed, t_layers, t_head;
+    int lazy;          /* orc_model_create_lazy: one layer of weights, regenerated per layer in forward */
+    uint32_t seed;     /* lazy: the synthetic weights' seed and mode */
+    int wmode;
+    int cur_layer;     /* lazy: layer whose weights the [0] buffers hold (-1: none) */
 };
+
+/* ---- synthetic weight generation over host threads (test-infrastructure speed only: every element is a
+ * pure function of its index, so the values do not depend on the thread count; the forward pass itself
+ * stays single-threaded, as the reference CPU path) */
+typedef struct {
+    float* dst;
+    uint64_t lo, hi;
+    uint32_t seed, stream;
+    float c, offset;
+    int wmode, rows_mode; /* rows_mode: lo/hi are rows of `cols` (apply_wmode), else elements (fill) */
+    int cols;
+} gen_job;
+
+static int gen_threads(uint64_t work) {
+    if (work < ((uint64_t)1 << 22)) return 1;
+    const char* e = getenv("ORC_GEN_THREADS");
+    long n = e ? atol(e) : sysconf(_SC_NPROCESSORS_ONLN);
+    if (n < 1) n = 1;
+    if (n > 32) n = 32;
+    return (int)n;
+}
+
+static void apply_wmode_rows(float* w, int r0, int r1, int cols, int wmode);
+
+static void* gen_worker(void* p) {
+    gen_job* j = (gen_job*)p;
+    if (j->rows_mode) {
+        apply_wmode_rows(j->dst, (int)j->lo, (int)j->hi, j->cols, j->wmode);
+    } else {
+        for (uint64_t i = j->lo; i < j->hi; i++) {
+            float v = (float)sli_rng_ih4(j->seed, j->stream, i) * j->c;
+            j->dst[i] = j->offset != 0.0f ? j->offset + v : v;
+        }
+    }
+    return NULL;
+}
+
+static void gen_run(gen_job proto, uint64_t n) {
+    int nt = gen_threads(proto.rows_mode ? n * (uint64_t)proto.cols : n);
+    pthread_t th[32];
+    gen_job jobs[32];
+    for (int t = 0; t < nt; t++) {
+        jobs[t] = proto;
+        jobs[t].lo = n * (uint64_t)t / (uint64_t)nt;
+        jobs[t].hi = n * (uint64_t)(t + 1) / (uint64_t)nt;
+        if (nt == 1 || pthread_create(&th[t], NULL, gen_worker, &jobs[t]) != 0) {
+            gen_worker(&jobs[t]);
+            th[t] = 0;
+        }
+    }
+    for (int t = 0; t < nt; t++)
+        if (th[t]) pthread_join(th[t], NULL);
+}
 
 static float** alloc_tab(int n, size_t each) {
     float** t = (float**)calloc((size_t)n, sizeof(float*));
@@ -242,22 +301,25 @@ static void free_tab(float** t, int n) {
     free(t);
 }
 
-orc_model* orc_model_create(const orc_config* cfg) {
+static orc_model* model_create(const orc_config* cfg, int lazy) {
     orc_model* m = (orc_model*)calloc(1, sizeof(orc_model));
     m->c = *cfg;
     const orc_config* c = &m->c;
     int L = c->n_layers, D = c->dim, I = c->ffn, V = c->vocab, T = c->max_len;
     m->kv_dim = c->n_kv_heads * c->head_dim;
     int KV = m->kv_dim;
+    m->lazy = lazy;
+    m->cur_layer = -1;
+    int LW = lazy ? 1 : L; /* lazy: one buffer set, regenerated layer by layer */
     m->emb = (float*)calloc((size_t)V * D, sizeof(float));
     m->norm = alloc_tab(2 * L + 1, (size_t)D);
-    m->wq = alloc_tab(L, (size_t)D * D);
-    m->wk = alloc_tab(L, (size_t)KV * D);
-    m->wv = alloc_tab(L, (size_t)KV * D);
-    m->wo = alloc_tab(L, (size_t)D * D);
-    m->up = alloc_tab(L, (size_t)I * D);
-    m->gate = alloc_tab(L, (size_t)I * D);
-    m->down = alloc_tab(L, (size_t)D * I);
+    m->wq = alloc_tab(LW, (size_t)D * D);
+    m->wk = alloc_tab(LW, (size_t)KV * D);
+    m->wv = alloc_tab(LW, (size_t)KV * D);
+    m->wo = alloc_tab(LW, (size_t)D * D);
+    m->up = alloc_tab(LW, (size_t)I * D);
+    m->gate = alloc_tab(LW, (size_t)I * D);
+    m->down = alloc_tab(LW, (size_t)D * I);
     m->kcache = (float*)calloc((size_t)L * T * KV, sizeof(float));
     m->vcache = (float*)calloc((size_t)L * T * KV, sizeof(float));
     m->x = (float*)calloc((size_t)D, 4);
@@ -277,18 +339,26 @@ orc_model* orc_model_create(const orc_config* cfg) {
     return m;
 }
 
+orc_model* orc_model_create(const orc_config* cfg) { return model_create(cfg, 0); }
+
+/* Full-size models (e.g. the 32-layer 7B step, 27 GB of fp32 weights) without holding every layer: the
+ * forward regenerates each layer's weights (bit-identical to orc_model_init_synthetic's) before using them.
+ * orc_model_weight serves only the embedding and norms of such a model. */
+orc_model* orc_model_create_lazy(const orc_config* cfg) { return model_create(cfg, 1); }
+
 void orc_model_free(orc_model* m) {
     if (!m) return;
     int L = m->c.n_layers;
     free(m->emb);
+    int LW = m->lazy ? 1 : L;
     free_tab(m->norm, 2 * L + 1);
-    free_tab(m->wq, L);
-    free_tab(m->wk, L);
-    free_tab(m->wv, L);
-    free_tab(m->wo, L);
-    free_tab(m->up, L);
-    free_tab(m->gate, L);
-    free_tab(m->down, L);
+    free_tab(m->wq, LW);
+    free_tab(m->wk, LW);
+    free_tab(m->wv, LW);
+    free_tab(m->wo, LW);
+    free_tab(m->up, LW);
+    free_tab(m->gate, LW);
+    free_tab(m->down, LW);
     free(m->kcache);
     free(m->vcache);
     free(m->x);
@@ -308,6 +378,7 @@ void orc_model_free(orc_model* m) {
 }
 
 float* orc_model_weight(orc_model* m, int kind, int index) {
+    if (m->lazy && kind != SLI_T_EMB && kind != SLI_T_NORM) return NULL;
     switch (kind) {
         case SLI_T_EMB: return m->emb;
         case SLI_T_NORM: return m->norm[index];
@@ -322,13 +393,12 @@ float* orc_model_weight(orc_model* m, int kind, int index) {
     }
 }
 
-static void apply_wmode(float* w, int rows, int cols, int wmode) {
-    size_t n = (size_t)rows * cols;
+static void apply_wmode_rows(float* w, int r0, int r1, int cols, int wmode) {
     if (wmode == ORC_W_F16) {
-        for (size_t i = 0; i < n; i++) w[i] = orc_round_f16(w[i]);
+        for (size_t i = (size_t)r0 * cols; i < (size_t)r1 * cols; i++) w[i] = orc_round_f16(w[i]);
     } else if (wmode == ORC_W_I8) {
         int8_t* q = (int8_t*)malloc((size_t)cols);
-        for (int r = 0; r < rows; r++) {
+        for (int r = r0; r < r1; r++) {
             float s;
             float* row = w + (size_t)r * cols;
             orc_quant_row_i8(row, cols, q, &s);
@@ -338,31 +408,54 @@ static void apply_wmode(float* w, int rows, int cols, int wmode) {
     }
 }
 
-int orc_model_init_synthetic(orc_model* m, uint32_t seed, int wmode) {
+static void apply_wmode(float* w, int rows, int cols, int wmode) {
+    if (wmode != ORC_W_F16 && wmode != ORC_W_I8) return;
+    gen_job j = {w, 0, 0, 0, 0, 0.0f, 0.0f, wmode, 1, cols};
+    gen_run(j, (uint64_t)rows);
+}
+
+/* orc_synth_fill over host threads (same values) */
+static void synth_fill(float* dst, uint64_t n, uint32_t seed, uint32_t stream, float c, float offset) {
+    gen_job j = {dst, 0, 0, seed, stream, c, offset, 0, 0, 0};
+    gen_run(j, n);
+}
+
+/* layer l's seven matrices into the given buffers (model.cpp:366-398 shapes) */
+static void gen_layer(orc_model* m, int l, float* wq, float* wk, float* wv, float* wo, float* up, float* gate,
+                      float* down) {
     const orc_config* c = &m->c;
-    int L = c->n_layers, D = c->dim, I = c->ffn, V = c->vocab, KV = m->kv_dim;
+    int D = c->dim, I = c->ffn, KV = m->kv_dim;
+    uint32_t seed = m->seed;
     float cD = SLI_SYNTH_C(1.0 / sqrt((double)D));
     float cI = SLI_SYNTH_C(1.0 / sqrt((double)I));
-    orc_synth_fill(m->emb, (uint64_t)V * D, seed, sli_stream_id(SLI_T_EMB, 0), SLI_SYNTH_C(0.02), 0.0f);
+    synth_fill(wq, (uint64_t)D * D, seed, sli_stream_id(SLI_T_WQ, l), cD, 0.0f);
+    synth_fill(wk, (uint64_t)KV * D, seed, sli_stream_id(SLI_T_WK, l), cD, 0.0f);
+    synth_fill(wv, (uint64_t)KV * D, seed, sli_stream_id(SLI_T_WV, l), cD, 0.0f);
+    synth_fill(wo, (uint64_t)D * D, seed, sli_stream_id(SLI_T_WO, l), cD, 0.0f);
+    synth_fill(up, (uint64_t)I * D, seed, sli_stream_id(SLI_T_UP, l), cD, 0.0f);
+    synth_fill(gate, (uint64_t)I * D, seed, sli_stream_id(SLI_T_GATE, l), cD, 0.0f);
+    synth_fill(down, (uint64_t)D * I, seed, sli_stream_id(SLI_T_DOWN, l), cI, 0.0f);
+    apply_wmode(wq, D, D, m->wmode);
+    apply_wmode(wk, KV, D, m->wmode);
+    apply_wmode(wv, KV, D, m->wmode);
+    apply_wmode(wo, D, D, m->wmode);
+    apply_wmode(up, I, D, m->wmode);
+    apply_wmode(gate, I, D, m->wmode);
+    apply_wmode(down, D, I, m->wmode);
+}
+
+int orc_model_init_synthetic(orc_model* m, uint32_t seed, int wmode) {
+    const orc_config* c = &m->c;
+    int L = c->n_layers, D = c->dim, V = c->vocab;
+    m->seed = seed;
+    m->wmode = wmode;
+    m->cur_layer = -1;
+    synth_fill(m->emb, (uint64_t)V * D, seed, sli_stream_id(SLI_T_EMB, 0), SLI_SYNTH_C(0.02), 0.0f);
     apply_wmode(m->emb, V, D, wmode);
     for (int i = 0; i < 2 * L + 1; i++)
         orc_synth_fill(m->norm[i], (uint64_t)D, seed, sli_stream_id(SLI_T_NORM, i), SLI_SYNTH_C(0.1), 1.0f);
-    for (int l = 0; l < L; l++) {
-        orc_synth_fill(m->wq[l], (uint64_t)D * D, seed, sli_stream_id(SLI_T_WQ, l), cD, 0.0f);
-        orc_synth_fill(m->wk[l], (uint64_t)KV * D, seed, sli_stream_id(SLI_T_WK, l), cD, 0.0f);
-        orc_synth_fill(m->wv[l], (uint64_t)KV * D, seed, sli_stream_id(SLI_T_WV, l), cD, 0.0f);
-        orc_synth_fill(m->wo[l], (uint64_t)D * D, seed, sli_stream_id(SLI_T_WO, l), cD, 0.0f);
-        orc_synth_fill(m->up[l], (uint64_t)I * D, seed, sli_stream_id(SLI_T_UP, l), cD, 0.0f);
-        orc_synth_fill(m->gate[l], (uint64_t)I * D, seed, sli_stream_id(SLI_T_GATE, l), cD, 0.0f);
-        orc_synth_fill(m->down[l], (uint64_t)D * I, seed, sli_stream_id(SLI_T_DOWN, l), cI, 0.0f);
-        apply_wmode(m->wq[l], D, D, wmode);
-        apply_wmode(m->wk[l], KV, D, wmode);
-        apply_wmode(m->wv[l], KV, D, wmode);
-        apply_wmode(m->wo[l], D, D, wmode);
-        apply_wmode(m->up[l], I, D, wmode);
-        apply_wmode(m->gate[l], I, D, wmode);
-        apply_wmode(m->down[l], D, I, wmode);
-    }
+    if (m->lazy) return 0; /* layers: regenerated in the forward */
+    for (int l = 0; l < L; l++) gen_layer(m, l, m->wq[l], m->wk[l], m->wv[l], m->wo[l], m->up[l], m->gate[l], m->down[l]);
     return 0;
 }
 
@@ -370,10 +463,40 @@ void orc_model_set_kv_f16(orc_model* m, int on) { m->kv_f16 = on; }
 float* orc_model_kcache(orc_model* m) { return m->kcache; }
 float* orc_model_vcache(orc_model* m) { return m->vcache; }
 
+typedef struct {
+    orc_model* m;
+    uint32_t seed;
+    int upto, l0, l1;
+} kv_job;
+static void fill_kv_layers(orc_model* m, uint32_t seed, int upto, int l0, int l1);
+static void* kv_worker(void* p) {
+    kv_job* j = (kv_job*)p;
+    fill_kv_layers(j->m, j->seed, j->upto, j->l0, j->l1);
+    return NULL;
+}
+
+/* one layer per host thread (test-infrastructure speed; the values do not depend on the split) */
 void orc_model_fill_kv_synthetic(orc_model* m, uint32_t seed, int upto) {
+    int L = m->c.n_layers;
+    int nt = gen_threads((uint64_t)L * upto * m->kv_dim);
+    if (nt > L) nt = L;
+    pthread_t th[32];
+    kv_job jobs[32];
+    for (int t = 0; t < nt; t++) {
+        jobs[t] = (kv_job){m, seed, upto, L * t / nt, L * (t + 1) / nt};
+        if (nt == 1 || pthread_create(&th[t], NULL, kv_worker, &jobs[t]) != 0) {
+            kv_worker(&jobs[t]);
+            th[t] = 0;
+        }
+    }
+    for (int t = 0; t < nt; t++)
+        if (th[t]) pthread_join(th[t], NULL);
+}
+
+static void fill_kv_layers(orc_model* m, uint32_t seed, int upto, int l0, int l1) {
     int KV = m->kv_dim, T = m->c.max_len;
     float c1 = SLI_SYNTH_C(1.0);
-    for (int l = 0; l < m->c.n_layers; l++) {
+    for (int l = l0; l < l1; l++) {
         for (int t = 0; t < upto; t++) {
             for (int j = 0; j < KV; j++) {
                 uint64_t idx = (uint64_t)t * KV + j;
@@ -406,12 +529,20 @@ int orc_model_forward(orc_model* m, int token, int pos, float* logits_out) {
     if (orc_embedding(token, m->emb, m->x, V, D) != 0) return -1; /* :48 */
     double t1 = now_s();
     for (int l = 0; l < L; l++) {
+        int lw = l; /* weight slot */
+        if (m->lazy) {
+            lw = 0;
+            if (m->cur_layer != l) {
+                gen_layer(m, l, m->wq[0], m->wk[0], m->wv[0], m->wo[0], m->up[0], m->gate[0], m->down[0]);
+                m->cur_layer = l;
+            }
+        }
         orc_rmsnorm(m->x, m->norm[2 * l], m->h, D, c->eps);          /* :52 */
         float* krow = m->kcache + ((size_t)l * T + pos) * KV;        /* :54-55 slice_KV_cache */
         float* vrow = m->vcache + ((size_t)l * T + pos) * KV;
-        orc_matmul(m->h, m->wq[l], m->q, D, D, 1.0f);                /* :58 */
-        orc_matmul(m->h, m->wk[l], krow, KV, D, 1.0f);               /* :60 */
-        orc_matmul(m->h, m->wv[l], vrow, KV, D, 1.0f);               /* :62 */
+        orc_matmul(m->h, m->wq[lw], m->q, D, D, 1.0f);                /* :58 */
+        orc_matmul(m->h, m->wk[lw], krow, KV, D, 1.0f);               /* :60 */
+        orc_matmul(m->h, m->wv[lw], vrow, KV, D, 1.0f);               /* :62 */
         orc_rope(m->q, krow, pos, m->sin_c, m->cos_c, D, KV, c->head_dim); /* :66-67 */
         if (m->kv_f16) {
             for (int j = 0; j < KV; j++) {
@@ -421,13 +552,13 @@ int orc_model_forward(orc_model* m, int token, int pos, float* logits_out) {
         }
         orc_mha(m->q, m->score, m->kcache, m->vcache, m->attn, l, pos, T, c->head_dim, c->n_heads,
                 c->n_kv_heads);                                       /* :70-78 */
-        orc_matmul(m->attn, m->wo[l], m->o, D, D, 1.0f);             /* :80-83 */
+        orc_matmul(m->attn, m->wo[lw], m->o, D, D, 1.0f);             /* :80-83 */
         orc_add(m->x, m->o, m->x1, D);                               /* :86-90 */
         orc_rmsnorm(m->x1, m->norm[2 * l + 1], m->h, D, c->eps);     /* :93-96 */
-        orc_matmul(m->h, m->up[l], m->u, I, D, 1.0f);                /* :99-102 */
-        orc_matmul(m->h, m->gate[l], m->g, I, D, 1.0f);              /* :105-108 */
+        orc_matmul(m->h, m->up[lw], m->u, I, D, 1.0f);                /* :99-102 */
+        orc_matmul(m->h, m->gate[lw], m->g, I, D, 1.0f);              /* :105-108 */
         orc_swiglu(m->u, m->g, m->a, I);                             /* :111-115 */
-        orc_matmul(m->a, m->down[l], m->f, D, I, 1.0f);              /* :118-121 */
+        orc_matmul(m->a, m->down[lw], m->f, D, I, 1.0f);              /* :118-121 */
         orc_add(m->f, m->x1, m->x, D);                               /* :124-128 */
     }
     double t2 = now_s();
@@ -478,6 +609,7 @@ static int wr(FILE* f, const float* p, size_t n) { return fwrite(p, sizeof(float
 /* model.cpp:336-469 order: embed, 2L+1 norms, wq[L], wk[L], wv[L], wo[L], up[L], gate[L], down[L]. */
 int orc_model_write_flat(const orc_model* m, const char* path) {
     const orc_config* c = &m->c;
+    if (m->lazy) return -2; /* its layers are not held */
     int L = c->n_layers, D = c->dim, I = c->ffn, V = c->vocab, KV = m->kv_dim;
     FILE* f = fopen(path, "wb");
     if (!f) return -1;

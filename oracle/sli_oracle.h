@@ -58,6 +58,8 @@ enum { ORC_W_F32 = 0, ORC_W_F16 = 1, ORC_W_I8 = 2 };
 
 typedef struct orc_model orc_model;
 orc_model* orc_model_create(const orc_config* cfg);
+/* full-size models: one layer of weights held, regenerated per layer inside orc_model_forward (same values) */
+orc_model* orc_model_create_lazy(const orc_config* cfg);
 void orc_model_free(orc_model* m);
 /* weight mode: values are generated in fp32 and then rounded (F16) or per-row quantised+dequantised
  * (I8) so the oracle computes in fp32 on exactly the weights the device holds. */

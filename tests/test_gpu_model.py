@@ -108,6 +108,32 @@ def test_llama7b_full_properties(gpu):
     gm.close()
 
 
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("w", ["f16", "i8"])
+def test_llama7b_full_32_layers_matches_oracle(gpu, oracle, w):
+    """The whole bench workload (C1: Llama-2-7B, 32 layers, full vocab, ctx 2048, step at pos 2047 over
+    KV rows 0..2046) against the oracle's full forward — the lazy oracle regenerates each layer's weights
+    in turn (27 GB of fp32 weights are never held). fp16 weights (C1) and int8 (C3). Bar: logits within
+    the north-star 1e-3 and the same argmax."""
+    from simplellminference_amd.model import LlamaModel, preset
+    cfg = preset("llama2-7b")
+    gm = LlamaModel(config=cfg, w_dtype=w, kv_dtype="f16", seed=1).init()
+    gm.fill_kv_synthetic(7, 2047)
+    got = gm.forward(1234, 2047)
+    gm.close()
+    om = oracle.Model(oracle.Config(cfg.vocab_size, cfg.hidden_size, cfg.num_attention_heads,
+                                    cfg.num_key_value_heads, cfg.head_dim, cfg.intermediate_size,
+                                    cfg.num_hidden_layers, cfg.max_length, cfg.rms_norm_eps, cfg.rope_theta),
+                      seed=1, wmode={"f16": oracle.W_F16, "i8": oracle.W_I8}[w], kv_f16=True, lazy=True)
+    om.fill_kv_synthetic(7, 2047)
+    want = om.forward(1234, 2047)
+    om.close()
+    err = float(np.abs(got - want).max())
+    print(f"32-layer 7B {w}: max|dlogit| {err:.3e}, |logit| max {np.abs(want).max():.3f}")
+    assert err <= 1e-3
+    assert int(np.argmax(got)) == int(np.argmax(want))
+
+
 def test_short_context_many_heads(gpu, oracle):
     """Llama-2-7B heads (32 x 128, fused QKV rows 12288) with max_length 64: the QKV epilogue's entry
     prefetch must stay inside the [T][hd/2] RoPE table (64 x 64 floats < 12288 rows)."""

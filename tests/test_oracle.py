@@ -182,3 +182,20 @@ def test_argmax_special_values_follow_max_element(oracle):
     for c in cases:
         x = np.array(c, np.float32)
         assert oracle.argmax(x) == _max_element(x), c
+
+
+def test_lazy_layers_match_eager(oracle):
+    """orc_model_create_lazy (one layer of weights held, each layer regenerated inside the forward, over host
+    threads) gives the eager model's logits bit for bit: f32 / f16 / int8 weights, MHA and GQA, two steps."""
+    import numpy as np
+    for (d, h, kvh, ffn), wm in [((64, 4, 4, 96), oracle.W_F32), ((64, 4, 2, 96), oracle.W_F16),
+                                 ((128, 4, 1, 160), oracle.W_I8)]:
+        cfg = oracle.Config(300, d, h, kvh, d // h, ffn, 3, 32, 1e-5, 10000.0)
+        outs = []
+        for lazy in (False, True):
+            m = oracle.Model(cfg, seed=5, wmode=wm, kv_f16=True, lazy=lazy)
+            m.fill_kv_synthetic(3, 20)
+            outs.append([m.forward(7, 20), m.forward(11, 21)])
+            m.close()
+        for a, b in zip(*outs):
+            assert np.array_equal(a, b)
