@@ -118,6 +118,25 @@ def test_group_c2_shard_shapes(gpu, c2_oracle, w, world):
     assert int(np.argmax(got)) == int(np.argmax(want[w]))
 
 
+@pytest.mark.timeout(600)
+def test_group_c2_full_model_tp8(gpu, oracle):
+    """BASELINE configs[2] end to end on one GPU: the whole 32-layer Llama-2-7B fp16 step (ctx 2048, pos 2047)
+    sharded over 8 in-process ranks (rank-order sums in place of the all-reduces), against the unsharded
+    lazy oracle (each layer's weights regenerated in turn)."""
+    from simplellminference_amd.model import TPGroup, preset
+    cfg = preset("llama2-7b")
+    g = TPGroup(cfg, 8, w_dtype="f16", kv_dtype="f16", seed=1).init()
+    g.fill_kv_synthetic(7, 2047)
+    got = g.forward(1234, 2047)
+    g.close()
+    om = oracle.Model(_ocfg(oracle, cfg), seed=1, wmode=oracle.W_F16, kv_f16=True, lazy=True)
+    om.fill_kv_synthetic(7, 2047)
+    want = om.forward(1234, 2047)
+    om.close()
+    assert np.abs(got - want).max() <= 1e-3, np.abs(got - want).max()
+    assert int(np.argmax(got)) == int(np.argmax(want))
+
+
 C4_TOKENS = [1234 + 9001 * b for b in range(8)]
 C4_POS = [4095, 4095, 100, 2047, 4000, 1, 3333, 4095]
 
