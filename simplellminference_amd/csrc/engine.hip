@@ -581,7 +581,8 @@ struct StepRecorder {
     // the LM head launch's grid (its workgroups each write one argmax key): gemv_lm's split and blocks
     static int lm_head_blocks(sli_model* m) {
         const int units = (m->v_n + 1) / 2;
-        return gemv_blocks(units, gemv_split<WT, 4>(units, m->D).cs);
+        const int cs = gemv_split<WT, 4>(units, m->D).cs;
+        return cs == 1 ? gemv_balanced_blocks(units) : gemv_blocks(units, cs);  // launch_gemv's grid
     }
     static int gemv_lm(sli_model* m) {
         GemvIn in{m->x, m->norms + (size_t)(2 * m->L) * m->D, m->c.eps, m->D};

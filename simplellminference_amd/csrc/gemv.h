@@ -415,13 +415,13 @@ __global__ void __launch_bounds__(kGemvThreads) gemv_kernel(const WT* __restrict
 }
 
 // the wo GEMV with its input merged from the attention's split partials (XStageMerge)
-template <typename WT, int R, int U, bool NT, class Epi, int NS = 8>
+template <typename WT, int R, int U, bool NT, class Epi, int NS = 8, int NB = 2>
 __global__ void __launch_bounds__(kGemvThreads) gemv_merge_kernel(const WT* __restrict__ W, GemvIn in, Epi epi_in,
                                                                   AttnMergeIn am) {
     Epi epi = epi_in;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     XStageMerge<Vec16<WT>::N / 4, NS> stage{am};
-    gemv_block<WT, R, U, NT>(W, in, epi, stage, smem);
+    gemv_block<WT, R, U, NT, Epi, XStageMerge<Vec16<WT>::N / 4, NS>, NB>(W, in, epi, stage, smem);
 }
 
 // Row-by-row fallback for shapes the vector kernel cannot take (cols*sizeof(WT) not a multiple of 16
@@ -671,23 +671,50 @@ inline int gemv_blocks(int units, int csplit = 1) {
     return b < maxb ? (b > 0 ? b : 1) : maxb;
 }
 
+// Wave-balanced grid for unsplit launches. A wave owns whole units, so at the full grid the waves differ by one
+// unit, and when units / waves is far from an integer the waves with one unit fewer finish early and the
+// launch's tail streams on part of the chip (gate/up at 7B: 11008 units on 4096 waves = 2.69, 31 % of the
+// waves idle for the last third). The smallest grid at which no wave holds more units than at the full grid
+// gives every wave (nearly) the same count; it is taken when it keeps >= 7/8 of the workgroups, so each
+// CU's share of the HBM stream stays under its per-CU fetch rate (gate/up: 230 workgroups, 31.4 -> 29.0 us,
+// C1 358 -> 368 tok/s; qkv at 1.5 units per wave would need 192 workgroups: measured slower, 17.9 -> 20.5 us;
+// profiles/r3_gemv_balance_ab.txt). SLI_GEMV_BALANCE=0 keeps the full grid (A/B).
+inline int gemv_balanced_blocks(int units) {
+    static const bool on = [] {
+        const char* e = getenv("SLI_GEMV_BALANCE");
+        return !(e && e[0] == '0');
+    }();
+    const int b = gemv_blocks(units);
+    if (!on) return b;
+    const int w = kGemvThreads / 64;
+    const int k = (units + b * w - 1) / (b * w);  // most units of a wave at the full grid
+    const int g = (units + k * w - 1) / (k * w);
+    // only where the full grid's tail is real (>= 8 % more unit slots than units; the LM head's 2.4 % measured
+    // slower at 250 workgroups: 41.2 -> 43-44 us)
+    return (g < b && 8 * g >= 7 * b && 100LL * k * b * w >= 108LL * units) ? g : b;
+}
+
 // NS: split partials a thread loads with its input (every live split of a context up to NS * ppwg
 // positions in one batch; more splits are read from memory one by one during the merge)
-template <typename WT, int R, int U, bool NT, class Epi, int NS = 8>
+// weight steps in flight per wave while the merge staging runs (A/B knob)
+#ifndef SLI_WO_NB
+#define SLI_WO_NB 2
+#endif
+template <typename WT, int R, int U, bool NT, class Epi, int NS = 8, int NB = SLI_WO_NB>
 hipError_t launch_gemv_merge(const WT* W, const GemvIn& in, const Epi& epi, const AttnMergeIn& am, int units,
                              hipStream_t s) {
     if (in.csplit != 1) return hipErrorInvalidValue;  // the merge-staged wo GEMV runs unsplit
-    const int grid = gemv_blocks(units);
+    const int grid = gemv_balanced_blocks(units);
     const size_t lds = gemv_lds_bytes(in.cols) + sizeof(float) * gemv_res_floats(units, grid, R);
-    hipLaunchKernelGGL((gemv_merge_kernel<WT, R, U, NT, Epi, NS>), dim3(grid), dim3(kGemvThreads), lds, s, W, in, epi,
-                       am);
+    hipLaunchKernelGGL((gemv_merge_kernel<WT, R, U, NT, Epi, NS, NB>), dim3(grid), dim3(kGemvThreads), lds, s, W, in,
+                       epi, am);
     return hipGetLastError();
 }
 
 template <typename WT, int R, int U, bool NT, class Epi, int NB = 2, bool SPLIT = false>
 hipError_t launch_gemv(const WT* W, const GemvIn& in, const Epi& epi, int units, hipStream_t s) {
     if (!SPLIT && in.csplit != 1) return hipErrorInvalidValue;  // a split needs the SPLIT instantiation
-    const int grid = gemv_blocks(units, in.csplit);
+    const int grid = in.csplit == 1 ? gemv_balanced_blocks(units) : gemv_blocks(units, in.csplit);
     const size_t lds = gemv_lds_bytes(in.cols) + sizeof(float) * gemv_res_floats(units, grid, R, in.csplit);
     hipLaunchKernelGGL((gemv_kernel<WT, R, U, NT, Epi, NB, SPLIT>), dim3(grid), dim3(kGemvThreads), lds, s, W, in,
                        epi);

@@ -585,7 +585,6 @@ __global__ void __launch_bounds__(256) pf_attn_mfma_kernel(PfAttnArgs<__half> a,
     for (int t = 0; t < NT; ++t) o[t] = pf_float4{0.0f, 0.0f, 0.0f, 0.0f};
     float mx = -INFINITY, l = 0.0f;
     char* kimg = sm + wave * G::WAVE;
-    char* vimg = kimg + G::IMG;
     const unsigned kbase = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)kimg;
     const unsigned vbase = kbase + G::IMG;
     const __half* kc = a.kc + (size_t)kvh * a.T * HD;
