@@ -25,6 +25,7 @@ struct GemvIn {
     int cols;
     unsigned long long* stamps = nullptr;  // diagnostic (tools/gemv_lab): per-wave s_memrealtime x4
     int csplit = 1;  // column parts per unit (gemv_block): a unit's rows split over up to csplit waves
+    int cw = 16;     // waves per workgroup that stream (gemv_wave_count); the others only shadow loads
 };
 
 constexpr int kGemvThreads = 1024;  // one persistent 16-wave workgroup per CU: x staged once per CU
@@ -281,8 +282,13 @@ __device__ __forceinline__ void gemv_block(const WT* __restrict__ W, const GemvI
     const int CS = SPLIT ? in.csplit : 1;  // compile-time 1 unless the launch split the columns
     const int cpp = (cpr + CS - 1) / CS;  // chunks per part (a part past the row end is all masked)
     const int ni = (ue - ub) * CS;       // the workgroup's items
-    const int ib = (int)(((unsigned)wave * (unsigned)ni) / (unsigned)nwaves);
-    const int ie = (int)(((unsigned)(wave + 1) * (unsigned)ni) / (unsigned)nwaves);
+    // in.cw streaming waves share the items; a wave past them has none and repeats the loads of wave
+    // (wave - cw)'s first steps (L2 hits on lines in flight), so no load sits behind a branch
+    const int cw = in.cw;
+    const bool idle = wave >= cw;
+    const int wq = idle ? wave - cw : wave;
+    const int ib = (int)(((unsigned)wq * (unsigned)ni) / (unsigned)cw);
+    const int ie = idle ? ib : (int)(((unsigned)(wq + 1) * (unsigned)ni) / (unsigned)cw);
     const int nsteps = (ie - ib) * cpp;
     float* res = smem + kGemvLdsHead + in.cols;
 
@@ -694,6 +700,27 @@ inline int gemv_balanced_blocks(int units) {
     return (g < b && 8 * g >= 7 * b && 100LL * k * b * w >= 108LL * units) ? g : b;
 }
 
+// Streaming waves per workgroup: with u units per workgroup and 16 waves, waves hold ceil(u / 16) or one
+// fewer; when that leaves waves idle for a whole unit (qkv at 7B: 24 units per workgroup = 1.5 per wave,
+// half the waves stream for half the launch), ceil(u / k) waves of k units each can take all of them.
+// Measured (profiles/r3_gemv_balance_ab.txt): int8 qkv 12.8 -> 12.4 us with 12 waves of 2 units, C3 +0.8 %;
+// fp16 qkv 18.1 -> 21.2 us (12 waves keep 3/4 of the bytes in flight per CU, and fp16 needs them) — so
+// int8 weights only (the launch sites pass the weight type). SLI_GEMV_WAVES=0 keeps 16 (A/B).
+template <typename WT>
+inline int gemv_wave_count(int units, int grid) {
+    if (!std::is_same<WT, int8_t>::value) return kGemvThreads / 64;
+    static const bool on = [] {
+        const char* e = getenv("SLI_GEMV_WAVES");
+        return !(e && e[0] == '0');
+    }();
+    const int w = kGemvThreads / 64;
+    if (!on) return w;
+    const int upw = (units + grid - 1) / grid;  // most units of a workgroup
+    const int k = (upw + w - 1) / w;
+    const int c = (upw + k - 1) / k;
+    return c >= w / 2 ? c : w;
+}
+
 // NS: split partials a thread loads with its input (every live split of a context up to NS * ppwg
 // positions in one batch; more splits are read from memory one by one during the merge)
 // weight steps in flight per wave while the merge staging runs (A/B knob)
@@ -701,10 +728,12 @@ inline int gemv_balanced_blocks(int units) {
 #define SLI_WO_NB 2
 #endif
 template <typename WT, int R, int U, bool NT, class Epi, int NS = 8, int NB = SLI_WO_NB>
-hipError_t launch_gemv_merge(const WT* W, const GemvIn& in, const Epi& epi, const AttnMergeIn& am, int units,
+hipError_t launch_gemv_merge(const WT* W, const GemvIn& in_, const Epi& epi, const AttnMergeIn& am, int units,
                              hipStream_t s) {
-    if (in.csplit != 1) return hipErrorInvalidValue;  // the merge-staged wo GEMV runs unsplit
+    if (in_.csplit != 1) return hipErrorInvalidValue;  // the merge-staged wo GEMV runs unsplit
     const int grid = gemv_balanced_blocks(units);
+    GemvIn in = in_;
+    in.cw = gemv_wave_count<WT>(units, grid);
     const size_t lds = gemv_lds_bytes(in.cols) + sizeof(float) * gemv_res_floats(units, grid, R);
     hipLaunchKernelGGL((gemv_merge_kernel<WT, R, U, NT, Epi, NS, NB>), dim3(grid), dim3(kGemvThreads), lds, s, W, in,
                        epi, am);
@@ -712,9 +741,11 @@ hipError_t launch_gemv_merge(const WT* W, const GemvIn& in, const Epi& epi, cons
 }
 
 template <typename WT, int R, int U, bool NT, class Epi, int NB = 2, bool SPLIT = false>
-hipError_t launch_gemv(const WT* W, const GemvIn& in, const Epi& epi, int units, hipStream_t s) {
-    if (!SPLIT && in.csplit != 1) return hipErrorInvalidValue;  // a split needs the SPLIT instantiation
+hipError_t launch_gemv(const WT* W, const GemvIn& in_, const Epi& epi, int units, hipStream_t s) {
+    if (!SPLIT && in_.csplit != 1) return hipErrorInvalidValue;  // a split needs the SPLIT instantiation
+    GemvIn in = in_;
     const int grid = in.csplit == 1 ? gemv_balanced_blocks(units) : gemv_blocks(units, in.csplit);
+    in.cw = in.csplit == 1 ? gemv_wave_count<WT>(units, grid) : kGemvThreads / 64;
     const size_t lds = gemv_lds_bytes(in.cols) + sizeof(float) * gemv_res_floats(units, grid, R, in.csplit);
     hipLaunchKernelGGL((gemv_kernel<WT, R, U, NT, Epi, NB, SPLIT>), dim3(grid), dim3(kGemvThreads), lds, s, W, in,
                        epi);
