@@ -76,7 +76,9 @@ def parse():
     ap.add_argument("--greedy-steps", type=int, default=64, help="the greedy sanity run's length (profiling passes: 2)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample budget")
     ap.add_argument("--gemv-iters", type=int, default=20)
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r2d_gemv_traffic.json"))
+    ap.add_argument("--traffic-json", default=next(
+        (p for p in (os.path.join(ROOT, "profiles", f) for f in ("r3_gemv_traffic.json", "r2d_gemv_traffic.json"))
+         if os.path.exists(p)), os.path.join(ROOT, "profiles", "r3_gemv_traffic.json")))
     return ap.parse_args()
 
 

@@ -308,8 +308,18 @@ __device__ __forceinline__ void gemv_block(const WT* __restrict__ W, const GemvI
     };
     const int it_last = max(ie - 1, ib);
     const Pos last{it_last, min(ub + it_last / CS, nunits - 1), it_last - (it_last / CS) * CS, cpp - 1};
+    // A load past the wave's last step (its last round when the step count is not a multiple of NB, or the
+    // first rounds of a wave with fewer than NB steps) reads the matrix's first chunk instead of repeating its
+    // own last step: that repeat was issued after the first copy had landed, so it went back to HBM (int8
+    // down at 7B, 3 chunks per row: FETCH_SIZE 1.10x the algorithmic bytes), while the first chunk of the
+    // launch is L2-resident on every XCD after its first read. Unconditional either way (only the address
+    // is selected). SLI_GEMV_DUP_LOADS=1: the round-2 behaviour (A/B).
+#ifndef SLI_GEMV_DUP_LOADS
+#define SLI_GEMV_DUP_LOADS 0
+#endif
+    const Pos dummy = SLI_GEMV_DUP_LOADS ? last : Pos{0, 0, 0, 0};
     auto load_step = [&](const Pos& q, u32x4 (&w)[U][R]) {
-        const Pos& a = q.it > it_last ? last : q;
+        const Pos& a = q.it > it_last ? dummy : q;
         int rows[R];
         epi.rows(min(a.u, nunits - 1), rows);
         const int v = (a.p * cpp + a.cc) * CV + lane;
