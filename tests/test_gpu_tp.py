@@ -130,7 +130,7 @@ def test_tp_rank_of_c2_shapes_steps_nocomm(gpu, monkeypatch, w, world):
     m.close()
 
 
-def _oneshot_rank(rank, world, port, name, batch, q, mode="oneshot"):
+def _oneshot_rank(rank, world, port, name, batch, q, mode="oneshot", w="f16"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0",
                       SLI_DEBUG_NOCOMM="1")  # no RCCL communicator: the one-shot kernels are the only exchange
     import torch
@@ -141,7 +141,7 @@ def _oneshot_rank(rank, world, port, name, batch, q, mode="oneshot"):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         dev = rank % torch.cuda.device_count()
-        m = LlamaModel(config=preset(name), w_dtype="f16", kv_dtype="f16", tp_rank=rank, tp_size=world,
+        m = LlamaModel(config=preset(name), w_dtype=w, kv_dtype="f16", tp_rank=rank, tp_size=world,
                        device=dev, seed=0, batch=batch).init()
         tp.open_oneshot(m)
         m.set_allreduce(mode)
@@ -181,6 +181,30 @@ def test_oneshot_allreduce_two_processes(gpu, name, batch, mode):
     q = ctx.Queue()
     port = _port()
     procs = [ctx.Process(target=_oneshot_rank, args=(r, 2, port, name, batch, q, mode)) for r in range(2)]
+    for p in procs:
+        p.start()
+    status, toks, logits, err = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+    assert status == "ok", toks
+    assert err == 0
+    assert np.array_equal(toks, rtoks)
+    assert np.abs(logits - rlogits).max() <= 1e-3
+
+
+@pytest.mark.parametrize("name,world,mode,w", [("tiny-h8", 4, "fused", "f16"), ("tiny-h8", 4, "oneshot", "f16"),
+                                               ("tiny-gqa", 2, "fused", "i8")])
+def test_oneshot_allreduce_more_ranks(gpu, name, world, mode, w):
+    """The one-shot exchange (separate launch or fused into wo / down) between 4 rank processes on one GPU, and
+    the fused form with int8 weights: tokens identical to the TP = 1 engine, logits within 1e-3, no device error."""
+    from simplellminference_amd.model import LlamaModel, preset
+    ref = LlamaModel(config=preset(name), w_dtype=w, kv_dtype="f16", seed=0).init()
+    rtoks, rlogits = ref.predict(PROMPT, 16, want_logits=True)
+    ref.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_oneshot_rank, args=(r, world, port, name, 1, q, mode, w)) for r in range(world)]
     for p in procs:
         p.start()
     status, toks, logits, err = q.get(timeout=300)
