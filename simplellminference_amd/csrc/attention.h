@@ -53,6 +53,12 @@ __device__ __forceinline__ int attn_pos(const AttnArgs<KT>& a, int kvh) {
 // same for every WAVES; WAVES trades registers for latency hiding: 16 waves of 4 (MHA, GQA-2: each
 // wave starts computing as soon as its own few rows land, 4 waves per SIMD overlap), 8 waves of 8
 // (GQA-4) or 4 waves of 16 (GQA-8, whose G query heads need the register room of one wave per SIMD).
+// K/V rows are read once per step: non-temporal loads (MI355X_MICROARCH.md nt-weights row), round 3: C1
+// attention 8.89 -> 8.40 us (367.5 vs 362.5 tok/s), C4 37.4 -> 35.4 us (1737 vs 1720 tok/s); variant A/B in
+// profiles/r3_attn_nt_ab.txt. SLI_ATTN_NT=0: default cache policy.
+#ifndef SLI_ATTN_NT
+#define SLI_ATTN_NT 1
+#endif
 #ifndef SLI_ATTN_SLOTS
 #define SLI_ATTN_SLOTS 64
 #endif
@@ -119,13 +125,13 @@ __device__ __forceinline__ bool attn_publish(const AttnArgs<KT>& a, int kvh, int
 #pragma unroll
         for (int it = 0; it < kAttnNit; ++it) {
             const int t = min(t0 + it * RPI + sub, t_end - 1);  // clamp, never branch around a load
-            kr[it] = load16<false>(kb + (long long)t * a.pos_stride);
+            kr[it] = load16<SLI_ATTN_NT != 0>(kb + (long long)t * a.pos_stride);
         }
         auto load_v = [&]() {
 #pragma unroll
             for (int it = 0; it < kAttnNit; ++it) {
                 const int t = min(t0 + it * RPI + sub, t_end - 1);
-                vr[it] = load16<false>(vb + (long long)t * a.pos_stride);
+                vr[it] = load16<SLI_ATTN_NT != 0>(vb + (long long)t * a.pos_stride);
             }
         };
         // LATE_V: V is loaded once the scores are done, so K and V never occupy registers together
