@@ -37,6 +37,8 @@ struct AttnArgs {
     int cache_heads = 0;    // > 0: the cache holds cache_heads kv heads shared by every sequence (prefill lanes
                             // of one sequence): kv head kvh reads cache head kvh % cache_heads
     int ppwg = 0;           // context positions per workgroup split (0: AttnGeom's PPWG; attn_stream.h sets it)
+    int kv_group = 1;       // > 1: kv head kvh reads cache head kvh / kv_group (a GQA head group run as kv_group
+                            // narrower groups that share each K/V row through the L2, ops.hip mha_launch_hd)
     int defer_merge = 0;    // != 0: only write the workgroup partials (plain stores); the splits are merged
                             // after the launch: 1 by the consumer (the wo GEMV's input staging, gemv.h
                             // XStageMerge), 2 by attn_merge_kernel (mha_launch launches it)
@@ -118,7 +120,7 @@ __device__ __forceinline__ bool attn_publish(const AttnArgs<KT>& a, int kvh, int
         for (int e = 0; e < EPV; ++e) ov[g][e] = 0.0f;
     }
     if (live_wave) {
-        const int ch = a.cache_heads > 0 ? kvh % a.cache_heads : kvh;
+        const int ch = a.cache_heads > 0 ? kvh % a.cache_heads : kvh / a.kv_group;
         const KT* kb = a.k + (long long)ch * a.head_stride + li * EPV;
         const KT* vb = a.v + (long long)ch * a.head_stride + li * EPV;
         u32x4 kr[kAttnNit], vr[kAttnNit];

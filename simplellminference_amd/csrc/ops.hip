@@ -174,8 +174,22 @@ static int mha_launch_hd(const float* q, const KT* kc, const KT* vc, float* out,
                    seq_heads > 0 ? seq_heads : Hkv, pos_seq_stride};
     a.cache_heads = cache_heads;
     a.defer_merge = defer_merge;
+    int g = H / Hkv;
+    // GQA-4 as two GQA-2 groups per kv head (SLI_ATTN_GQA_SPLIT=2; 4: four MHA heads): the 59-VGPR GQA-2 kernel at 8 waves/SIMD
+    // instead of the 128-VGPR GQA-4 one at 4; the two groups of a kv head are wg_splits blocks apart and read
+    // the same K/V rows. Deferred merges only (partials are indexed by q head; the counters by kv head).
+    static const int gqa_split = [] {  // 2: two GQA-2 groups, 4: four MHA heads
+        const char* e = getenv("SLI_ATTN_GQA_SPLIT");
+        return e && (e[0] == '2' || e[0] == '4') ? e[0] - '0' : 1;
+    }();
+    if (gqa_split > 1 && g == 4 && defer_merge && cache_heads == 0) {
+        g /= gqa_split;
+        a.kv_group = gqa_split;
+        a.n_kv_heads = gqa_split * Hkv;
+        a.seq_heads *= gqa_split;
+        Hkv *= gqa_split;
+    }
     const int blocks = Hkv * wg_splits;
-    const int g = H / Hkv;
     switch (g) {
         case 1: hipLaunchKernelGGL((attn_partial_kernel<KT, HD, 1>), dim3(blocks), dim3(64 * attn_waves(1)), 0, s, a); break;
         case 2: hipLaunchKernelGGL((attn_partial_kernel<KT, HD, 2>), dim3(blocks), dim3(64 * attn_waves(2)), 0, s, a); break;
