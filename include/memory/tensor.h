@@ -2,6 +2,7 @@
 // fp32 by default (reference semantics), with an element-type extension for fp16 / int8 weights.
 #pragma once
 #include <memory>
+#include <numeric>  // std::accumulate, which the reference's source/op/layer.cpp:187 gets from here (tensor.h:7)
 #include <utility>
 #include <vector>
 
@@ -9,7 +10,12 @@
 
 namespace mem {
 
-class Tensor {
+// ABI tag: this Tensor carries an element type (dtype_) after the reference's fields, so it is 56 bytes where
+// the reference's include/memory/tensor.h Tensor is 48. The tag is part of every mangled name that takes a
+// Tensor (mem::Tensor[abi:sli_dtype]), so an object compiled against the REFERENCE's memory headers cannot
+// link against libsli.so's kernel::*_cuda launchers (an undefined-symbol error) instead of silently passing a
+// 48-byte object to code that reads 56. INTEGRATION.md Level 2: compile against this include/.
+class [[gnu::abi_tag("sli_dtype")]] Tensor {
 public:
     Tensor() = default;
     explicit Tensor(std::vector<int32_t> dims, bool need_alloc = false, std::shared_ptr<DeviceAllocator> alloc = nullptr,

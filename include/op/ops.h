@@ -56,8 +56,11 @@ private:
     int32_t pos_ = 0;
     int32_t max_seq_len_ = 0;
     int32_t head_dim_ = 0;
+    int32_t hidden_dim_ = 0;         // num_attention_heads * head_dim (mha.cpp:21, the reference's members)
+    int32_t kv_hidden_dim_ = 0;      // num_key_value_heads * head_dim (mha.cpp:22)
     int32_t num_attention_heads_ = 0;
     int32_t num_key_value_heads_ = 0;
+    int32_t att_kv_head_group_ = 0;  // num_attention_heads / num_key_value_heads (mha.cpp:23)
     mem::Tensor workspace_;  // split-context partials (replaces the reference's score scratch)
 };
 

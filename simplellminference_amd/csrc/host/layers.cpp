@@ -165,6 +165,9 @@ MultiHeadAttention::MultiHeadAttention(base::DeviceType d, int32_t max_seq_len, 
       num_key_value_heads_(num_key_value_heads) {
     reset_input_size(4);
     reset_output_size(1);
+    hidden_dim_ = num_attention_heads * head_dim;
+    kv_hidden_dim_ = num_key_value_heads * head_dim;
+    att_kv_head_group_ = num_key_value_heads > 0 ? num_attention_heads / num_key_value_heads : 0;
 }
 void MultiHeadAttention::set_pos(int32_t pos) { pos_ = pos; }
 void MultiHeadAttention::set_layer_index(int32_t index) { layer_index_ = index; }
