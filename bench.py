@@ -19,9 +19,10 @@ per launch / its mean launch time, measured live with HIP events on the engine's
 (sli_model_time_families); `roofline.families` lists every family the same way, and `roofline.traffic`
 is that kernel's HBM bytes per launch from the committed rocprofv3 FETCH_SIZE pass (x2 gfx950
 correction). `greedy_64` is a true 64-token greedy decode (positions ctx-64 .. ctx-1, the state advancing
-on the device) beside the idempotent-step timing. `cpu_baseline` times the C oracle (single-threaded
-restatement of the reference CPU path) pinned to one host core, on a bounded sample, and projects the
-full model's tokens/s.
+on the device) beside the idempotent-step timing. `cpu_baseline` times the reference's own CPU path
+(oracle/_ref/libref.so, compiled from the reference sources in the build container) pinned to one host
+core on a bounded 2-layer sample and projects the full model's tokens/s; beside it the oracle port on one
+core and on all cores (labelled not reference).
 """
 from __future__ import annotations
 
@@ -38,7 +39,6 @@ sys.path.insert(0, ROOT)
 METRIC = "decode tokens/sec, Llama-7B fp16 seq=1 ctx=2048, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 CTX = 2048
-CPU_CALIBRATION = round(0.619 / 0.439, 3)  # port / reference CPU step time on the probe shape
 FAMILY_KERNELS = {
     False: {"step": "ps_step_kernel (the whole decode step as one persistent launch: 5 phases x 32 layers + LM head)",
             "qkv": "gemv_kernel<EpiQKV> (RMSNorm + [wq;wk;wv] GEMV + RoPE + K/V write)",
@@ -82,52 +82,87 @@ def parse():
     return ap.parse_args()
 
 
+def _time_steps(fwd, timing, n_layers, budget_s, min_steps=3, max_steps=50):
+    """Median embed / per-layer / head seconds of repeated forwards (at least min_steps, then until the budget)."""
+    t_emb, t_lay, t_head = [], [], []
+    t0 = time.perf_counter()
+    while len(t_lay) < max_steps:
+        fwd()
+        e, l, h = timing()
+        t_emb.append(e)
+        t_lay.append(l)
+        t_head.append(h)
+        if len(t_lay) >= min_steps and time.perf_counter() - t0 >= budget_s:
+            break
+    return statistics.median(t_emb), statistics.median(t_lay) / n_layers, statistics.median(t_head), len(t_lay)
+
+
 def cpu_baseline(budget_s: float, preset_name: str = "llama2-7b", ctx: int = CTX) -> dict:
-    """Oracle (port of the reference CPU path, 1 thread, one sequence at a time): a 2-layer model of the
-    workload's shape with its full tied LM head at position ctx-1; full-model time = embed + L * layer + head."""
+    """The host-CPU baseline, timed on this box's cores in this run.
+
+    `value`: the REFERENCE's own CPU path — oracle/_ref/libref.so, its source/kernel/cpu + source/op compiled in
+    place from the reference sources in the build container (oracle/Makefile `ref`), the ops wired as
+    model.cpp:40-140 (oracle/ref_harness.cpp) — on 1 pinned core, one sequence per step as the reference; a
+    2-layer model of the workload's shape with its full tied LM head at position ctx-1 (KV rows 0..ctx-2 filled),
+    the full model's step projected as embed + L x layer + head. If libref.so is absent: the oracle port instead
+    (kind "port"). Beside it, on the same sample: the port on 1 core (the measured port / reference ratio, no
+    factor applied anywhere) and the port with GEMV rows over all cores of this process ("all_cores", labelled
+    not reference)."""
     import oracle as O
+    from oracle import ref as R
     from simplellminference_amd.model import preset
     pc = preset(preset_name, max_length=ctx)
     cfg = O.Config(pc.vocab_size, pc.hidden_size, pc.num_attention_heads, pc.num_key_value_heads, pc.head_dim,
                    pc.intermediate_size, 2, ctx, pc.rms_norm_eps, pc.rope_theta)
     n_layers = pc.num_hidden_layers
-    # pinned to one host core in-process (no re-exec): the reference CPU path is single-threaded
     prev = os.sched_getaffinity(0)
     core = max(prev)
-    os.sched_setaffinity(0, {core})
+    n_all = max(1, min(len(prev), int(os.environ.get("OMP_NUM_THREADS", len(prev))), 32))
     m = O.Model(cfg, seed=1, wmode=O.W_F32)
     m.fill_kv_synthetic(7, ctx - 1)
-    t_lay, t_head, t_emb = [], [], []
-    t0 = time.perf_counter()
-    while True:
-        m.forward(1234, ctx - 1)
-        e, l, h = m.last_timing()
-        t_emb.append(e)
-        t_lay.append(l / cfg.n_layers)
-        t_head.append(h)
-        if time.perf_counter() - t0 >= budget_s or len(t_lay) >= 50:
-            break
+
+    def run(label, fwd, timing, budget):
+        e, lay, h, n = _time_steps(fwd, timing, cfg.n_layers, budget)
+        step = e + n_layers * lay + h
+        return {"tokens_per_s": 1.0 / step, "step_s": step, "sample_step_s": e + cfg.n_layers * lay + h,
+                "layer_ms": lay * 1e3, "head_ms": h * 1e3, "steps": n, "label": label}
+
+    os.sched_setaffinity(0, {core})  # the reference CPU path is single-threaded: one pinned core, in-process
+    try:
+        ref = None
+        if os.path.exists(R.LIB_PATH):
+            rm = R.Model(cfg, flat=m.flat_image())
+            k, v = rm.kv_cache()
+            ok, ov = m.kv_cache()
+            k[:] = ok
+            v[:] = ov
+            ref = run("reference", lambda: rm.forward(1234, ctx - 1), rm.last_timing, 0.55 * budget_s)
+            rm.close()
+        port = run("port", lambda: m.forward(1234, ctx - 1), m.last_timing, (0.2 if ref else 0.75) * budget_s)
+    finally:
+        os.sched_setaffinity(0, prev)
+    m.set_threads(n_all)
+    allc = run("all cores", lambda: m.forward(1234, ctx - 1), m.last_timing, 0.2 * budget_s)
     m.close()
-    os.sched_setaffinity(0, prev)
-    layer, head, emb = statistics.median(t_lay), statistics.median(t_head), statistics.median(t_emb)
-    step = emb + n_layers * layer + head
-    sample_step = emb + 2 * layer + head
-    # Calibration against the reference's own CPU build (SURVEY §8(d): the port must time within 15 % of it):
-    # on the probe shape (2 Llama-2-7B layers + the 32000 x 4096 head) the reference took 0.439 s per step
-    # (SURVEY §6, ref_cpu_7b2l) and this port 0.619 s in the same container image (round 3, DESIGN.md §5).
-    # Both inner loops compile to the same dependent mulss/addss chain, so the port's step time is divided
-    # by the factor: `value` is the reference's projected speed, `value_port_measured` the port's own.
-    cal = CPU_CALIBRATION
-    return {"value": cal / step, "unit": "tokens/s", "cores": 1, "core_id": core, "kind": "port",
-            "value_port_measured": 1.0 / step, "calibration_factor": cal,
-            "calibration": ("port step time / reference step time on the probe shape in this container image "
-                            "(0.619 s / 0.439 s); value = port tokens/s x factor"),
-            "sample_step_s": round(sample_step, 4),
-            "sample": (f"C oracle (oracle/sli_oracle.c, fp32, 1 thread pinned to core {core}, one sequence per "
-                       f"step as the reference) on {len(t_lay)} decode steps of a 2-layer {preset_name}-shape model "
-                       f"(+{pc.vocab_size}x{pc.hidden_size} tied head) at pos {ctx - 1}: median {sample_step:.3f} s per "
-                       f"sample step (layer {layer * 1e3:.1f} ms, head {head * 1e3:.1f} ms); full {n_layers}-layer step "
-                       f"projected {step:.2f} s = embed + {n_layers} x layer + head")}
+    prim = ref or port
+    shape = (f"2-layer {preset_name}-shape model (+{pc.vocab_size}x{pc.hidden_size} tied head), fp32, at pos "
+             f"{ctx - 1} (KV rows 0..{ctx - 2} filled), one sequence per step; full {n_layers}-layer step "
+             f"projected = embed + {n_layers} x layer + head")
+    who = ("the reference CPU path (oracle/_ref/libref.so: source/kernel/cpu + source/op compiled from the reference "
+           "sources, the model.cpp op wiring)" if ref else "the C oracle port (oracle/sli_oracle.c)")
+    out = {"value": prim["tokens_per_s"], "unit": "tokens/s", "cores": 1, "core_id": core,
+           "kind": "reference" if ref else "port",
+           "sample": (f"{who}, 1 thread pinned to core {core}, {prim['steps']} steps of a {shape}: median "
+                      f"{prim['sample_step_s']:.3f} s per sample step (layer {prim['layer_ms']:.1f} ms, head "
+                      f"{prim['head_ms']:.1f} ms), full step {prim['step_s']:.2f} s"),
+           "port_1core": {"value": port["tokens_per_s"], "step_s": round(port["step_s"], 3),
+                          "layer_ms": round(port["layer_ms"], 2), "head_ms": round(port["head_ms"], 2)},
+           "all_cores": {"value": allc["tokens_per_s"], "unit": "tokens/s", "cores": n_all, "kind": "port",
+                         "label": "NOT the reference (single-threaded): the oracle port with GEMV rows split over "
+                                  f"{n_all} host threads, bit-identical results", "step_s": round(allc["step_s"], 3)}}
+    if ref:
+        out["port_over_reference_step_time"] = round(port["step_s"] / ref["step_s"], 3)
+    return out
 
 
 def _oneshot_opened(model, dist, torch, mode) -> bool:
@@ -371,7 +406,7 @@ def main():
         wb_el = {"f16": 2.0, "i8": 1.0, "f32": 4.0}[a.w_dtype]
         layer_bytes = wbytes - cfg.vocab_size * cfg.hidden_size * wb_el / world  # this rank's layer weights
         params = layer_bytes / wb_el
-        mfma = a.w_dtype in ("f16", "i8")
+        mfma = model.prefill_path() == "mfma"  # the path the engine took (sli_model_prefill_path)
         chunks = []  # (valid rows, padded rows) per chunk (engine.hip kPfSizes)
         for p0 in range(0, n - 1, 256):
             nv = min(256, n - 1 - p0)
@@ -401,7 +436,8 @@ def main():
                           "mfma_peak_tflops": 2500.0,
                           "path": ("MFMA pgemm (v_mfma_f32_16x16x32_f16, fp16 hi + lo activations), chunks of "
                                    "<= 256 positions, block-causal attention" if mfma
-                                   else "decode step, teacher-forced (no MFMA path for fp32 weights)"),
+                                   else "decode step, teacher-forced (sli_model_prefill_path = 0: fp32 weights, an "
+                                        "unsupported shard shape, or a TP rank without an RCCL communicator)"),
                           "vs_token_by_token_s": round((n - 1) * ms * 1e-3, 4)}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a.cpu_seconds, a.preset, a.ctx)

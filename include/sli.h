@@ -197,6 +197,9 @@ int sli_model_get_state_seq(sli_model* m, int32_t seq, int32_t* pos, int32_t* to
  * (token ids[n-1], position n-1, advancing, prompt = ids), so the next sli_model_step yields the first
  * greedy token exactly as the reference's token-by-token predict (model.cpp:157-165) would. */
 int sli_model_prefill(sli_model* m, const int32_t* ids, int32_t n);
+/* Which path sli_model_prefill takes for this model: 1 = chunked MFMA GEMMs (prefill.h), 0 = the decode step,
+ * teacher-forced (fp32 weights, batch > 1, unsupported shapes, or a TP rank without an RCCL communicator). */
+int sli_model_prefill_path(const sli_model* m);
 /* sli_model_predict with the prompt prefilled: tokens_out[t] as sli_model_predict; logits_out rows for
  * positions < n_prompt - 1 (not computed by the prefill) are NaN. */
 int sli_model_predict_prefill(sli_model* m, const int32_t* prompt, int32_t n_prompt, int32_t max_length,

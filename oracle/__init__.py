@@ -77,6 +77,7 @@ def lib():
         L.orc_model_predict.argtypes = [ctypes.c_void_p, I32P, ctypes.c_int, ctypes.c_int, I32P, F32P]
         L.orc_model_predict.restype = ctypes.c_int
         L.orc_model_last_timing.argtypes = [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_double)] * 3
+        L.orc_model_set_threads.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.orc_model_write_flat.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
         L.orc_model_write_flat.restype = ctypes.c_int
         _lib = L
@@ -277,6 +278,18 @@ class Model:
         a, b, c = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
         lib().orc_model_last_timing(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
         return a.value, b.value, c.value
+
+    def set_threads(self, n: int):
+        """GEMV rows over n host threads (bit-identical; the all-cores CPU line, not the reference)."""
+        lib().orc_model_set_threads(self._h, n)
+
+    def flat_image(self) -> np.ndarray:
+        """The reference's flat fp32 weight image (model.cpp:336-469 order) in memory."""
+        c = self.cfg
+        parts = [self.weight(T_EMB).ravel()] + [self.weight(T_NORM, i) for i in range(2 * c.n_layers + 1)]
+        for kind in (T_WQ, T_WK, T_WV, T_WO, T_UP, T_GATE, T_DOWN):
+            parts += [self.weight(kind, l).ravel() for l in range(c.n_layers)]
+        return np.concatenate(parts)
 
     def write_flat(self, path: str):
         if lib().orc_model_write_flat(self._h, path.encode()) != 0:

@@ -60,7 +60,11 @@ def lib():
         L.ref_argmax.restype = ctypes.c_int
         L.ref_model_create.argtypes = [ctypes.c_int] * 8 + [ctypes.c_float, ctypes.c_float, ctypes.c_char_p]
         L.ref_model_create.restype = ctypes.c_void_p
+        L.ref_model_create_mem.argtypes = [ctypes.c_int] * 8 + [ctypes.c_float, ctypes.c_float, F32P, ctypes.c_size_t]
+        L.ref_model_create_mem.restype = ctypes.c_void_p
         L.ref_model_free.argtypes = [ctypes.c_void_p]
+        L.ref_model_kv.argtypes = [ctypes.c_void_p, ctypes.POINTER(F32P), ctypes.POINTER(F32P)]
+        L.ref_model_last_timing.argtypes = [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_double)] * 3
         L.ref_model_forward.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, F32P]
         L.ref_model_predict.argtypes = [ctypes.c_void_p, I32P, ctypes.c_int, ctypes.c_int, I32P, F32P]
         L.ref_model_predict.restype = ctypes.c_int
@@ -149,17 +153,41 @@ class Model:
     """LlamaModel over the reference's op layers, weights from the reference's flat fp32 file
     (the oracle writes it: oracle.Model.write_flat)."""
 
-    def __init__(self, cfg, flat_path: str):
+    def __init__(self, cfg, flat_path: str | None = None, flat: np.ndarray | None = None):
+        """flat_path: the reference's flat fp32 weight file; or flat: the same image in memory (kept alive)."""
         self.cfg = cfg
-        self._h = lib().ref_model_create(cfg.vocab, cfg.dim, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, cfg.ffn,
-                                         cfg.n_layers, cfg.max_len, cfg.eps, cfg.theta, flat_path.encode())
+        self._flat = None
+        if flat is not None:
+            self._flat = np.ascontiguousarray(flat, np.float32)
+            self._h = lib().ref_model_create_mem(cfg.vocab, cfg.dim, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim,
+                                                 cfg.ffn, cfg.n_layers, cfg.max_len, cfg.eps, cfg.theta,
+                                                 _f(self._flat), self._flat.size)
+        else:
+            self._h = lib().ref_model_create(cfg.vocab, cfg.dim, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim,
+                                             cfg.ffn, cfg.n_layers, cfg.max_len, cfg.eps, cfg.theta,
+                                             flat_path.encode())
         if not self._h:
-            raise RuntimeError(f"ref_model_create failed for {flat_path}")
+            raise RuntimeError(f"ref_model_create failed ({flat_path or 'in-memory image'})")
+
+    def kv_cache(self):
+        """(K, V) caches as [L][T][KV] fp32 views of the model's own buffers."""
+        k, v = F32P(), F32P()
+        lib().ref_model_kv(self._h, ctypes.byref(k), ctypes.byref(v))
+        c = self.cfg
+        shape = (c.n_layers, c.max_len, c.n_kv_heads * c.head_dim)
+        n = int(np.prod(shape))
+        return (np.ctypeslib.as_array(k, (n,)).reshape(shape), np.ctypeslib.as_array(v, (n,)).reshape(shape))
+
+    def last_timing(self):
+        e, l, h = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        lib().ref_model_last_timing(self._h, ctypes.byref(e), ctypes.byref(l), ctypes.byref(h))
+        return e.value, l.value, h.value
 
     def close(self):
         if self._h:
             lib().ref_model_free(self._h)
             self._h = None
+        self._flat = None
 
     def __del__(self):
         try:

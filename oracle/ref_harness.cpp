@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <ctime>
 #include <map>
 #include <memory>
 #include <vector>
@@ -142,8 +143,15 @@ struct RefModel {
     std::shared_ptr<op::argmaxLayer> argmax;
     std::vector<LayerP> norms, wq, wk, wv, wo, up, gate, down;
     std::map<int, mem::Tensor> buf;
+    double t_emb = 0, t_layers = 0, t_head = 0;  // last forward, seconds (harness instrumentation)
     const mem::Tensor& get(Buf t) const { return buf.at(int(t)); }
 };
+
+double now_s() {
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
 
 void add_fp32(const mem::Tensor& a, const mem::Tensor& b, const mem::Tensor& out, int n) {
     const float* x = a.ptr<float>();
@@ -156,7 +164,9 @@ void add_fp32(const mem::Tensor& a, const mem::Tensor& b, const mem::Tensor& out
 void forward(RefModel& m) {
     const auto& c = m.c;
     int pos = const_cast<mem::Tensor&>(m.get(position)).index<int>(0);
+    const double t0 = now_s();
     m.emb->forward(m.get(input_token), m.get(emb_output));
+    const double t1 = now_s();
     for (int l = 0; l < c.num_hidden_layers; l++) {
         m.norms[2 * l]->forward(m.get(emb_output), m.get(rms_output));
         const auto& [key, value] =
@@ -177,8 +187,12 @@ void forward(RefModel& m) {
         m.down[l]->forward(m.get(swi_output), m.get(ffn_output));
         add_fp32(m.get(ffn_output), m.get(ffn_input), m.get(emb_output), c.hidden_size);
     }
+    const double t2 = now_s();
     m.norms[2 * c.num_hidden_layers]->forward(m.get(emb_output), m.get(rms_output));
     m.cls->forward(m.get(rms_output), m.get(model_pred));
+    m.t_emb = t1 - t0;
+    m.t_layers = t2 - t1;
+    m.t_head = now_s() - t2;
 }
 
 std::vector<LayerP> matmuls(RefModel& m, size_t& off, int rows, int cols) {
@@ -199,15 +213,12 @@ void ref_model_free(void* h);
 // model.cpp:22-39 init(): read_model_file (:203-245), create_param_layers (:323-469),
 // create_nonparam_layers (:312-321), init_mem (:246-310) — on the CPU device, config passed in (the
 // reference hard-codes config.h). Returns nullptr if the file cannot be mapped.
+static void* create(RefModel* m, int vocab, int dim, int n_heads, int n_kv_heads, int head_dim, int ffn,
+                    int n_layers, int max_len, float eps, float theta, size_t file_bytes);
+
 void* ref_model_create(int vocab, int dim, int n_heads, int n_kv_heads, int head_dim, int ffn, int n_layers,
                        int max_len, float eps, float theta, const char* path) {
     auto* m = new RefModel();
-    auto& c = m->c;
-    c.vocab_size = vocab; c.hidden_size = dim; c.num_attention_heads = n_heads; c.num_key_value_heads = n_kv_heads;
-    c.head_dim = head_dim; c.kv_hidden_size = n_kv_heads * head_dim; c.intermediate_size = ffn;
-    c.num_hidden_layers = n_layers; c.max_length = max_len; c.rms_norm_eps = eps; c.rope_theta = theta;
-    const auto cpu = base::DeviceType::kDeviceCPU;
-
     m->raw = std::make_shared<model::RawModelDataFp32>();
     int fd = open(path, O_RDONLY);
     struct stat sb;
@@ -217,6 +228,27 @@ void* ref_model_create(int vocab, int dim, int n_heads, int n_kv_heads, int head
     m->raw->weight_data = mmap(nullptr, sb.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
     m->raw->data = m->raw->weight_data;  // so ~RawModelData unmaps it (the reference leaves `data` unset)
     if (m->raw->weight_data == MAP_FAILED) { m->raw->data = nullptr; delete m; return nullptr; }
+    return create(m, vocab, dim, n_heads, n_kv_heads, head_dim, ffn, n_layers, max_len, eps, theta, sb.st_size);
+}
+
+// The same model over a flat fp32 image already in host memory (the caller keeps it alive): the CPU-baseline
+// leg builds it from the synthetic weights instead of writing a multi-GB file.
+void* ref_model_create_mem(int vocab, int dim, int n_heads, int n_kv_heads, int head_dim, int ffn, int n_layers,
+                           int max_len, float eps, float theta, const float* flat, size_t n_floats) {
+    auto* m = new RefModel();
+    m->raw = std::make_shared<model::RawModelDataFp32>();
+    m->raw->weight_data = const_cast<float*>(flat);
+    return create(m, vocab, dim, n_heads, n_kv_heads, head_dim, ffn, n_layers, max_len, eps, theta,
+                  n_floats * sizeof(float));
+}
+
+static void* create(RefModel* m, int vocab, int dim, int n_heads, int n_kv_heads, int head_dim, int ffn,
+                    int n_layers, int max_len, float eps, float theta, size_t file_bytes) {
+    auto& c = m->c;
+    c.vocab_size = vocab; c.hidden_size = dim; c.num_attention_heads = n_heads; c.num_key_value_heads = n_kv_heads;
+    c.head_dim = head_dim; c.kv_hidden_size = n_kv_heads * head_dim; c.intermediate_size = ffn;
+    c.num_hidden_layers = n_layers; c.max_length = max_len; c.rms_norm_eps = eps; c.rope_theta = theta;
+    const auto cpu = base::DeviceType::kDeviceCPU;
 
     size_t off = 0;
     m->emb = std::make_shared<op::EmbeddingLayer>(cpu, vocab, dim);
@@ -237,7 +269,7 @@ void* ref_model_create(int vocab, int dim, int n_heads, int n_kv_heads, int head
     m->up = matmuls(*m, off, ffn, dim);
     m->gate = matmuls(*m, off, ffn, dim);
     m->down = matmuls(*m, off, dim, ffn);
-    if (off * sizeof(float) > size_t(sb.st_size)) { ref_model_free(m); return nullptr; }
+    if (off * sizeof(float) > file_bytes) { ref_model_free(m); return nullptr; }
 
     m->argmax = std::make_shared<op::argmaxLayer>(cpu, vocab);
     m->mha = std::make_shared<op::MultiHeadAttention>(cpu, max_len, head_dim, n_heads, n_kv_heads);
@@ -260,6 +292,21 @@ void* ref_model_create(int vocab, int dim, int n_heads, int n_kv_heads, int head
 }
 
 void ref_model_free(void* h) { delete static_cast<RefModel*>(h); }
+
+// the model's K / V caches [L][T][KV] fp32 (model.cpp:264-265), e.g. to fill rows before timing a late position
+void ref_model_kv(void* h, float** k, float** v) {
+    auto& m = *static_cast<RefModel*>(h);
+    *k = const_cast<float*>(m.get(key_cache).ptr<float>());
+    *v = const_cast<float*>(m.get(value_cache).ptr<float>());
+}
+
+// seconds of the last forward: embedding, the transformer layers, final norm + LM head
+void ref_model_last_timing(void* h, double* t_emb, double* t_layers, double* t_head) {
+    auto& m = *static_cast<RefModel*>(h);
+    *t_emb = m.t_emb;
+    *t_layers = m.t_layers;
+    *t_head = m.t_head;
+}
 
 // one LlamaModel::forward with input_token = token, position = pos; logits [vocab]
 void ref_model_forward(void* h, int token, int pos, float* logits) {

@@ -235,6 +235,7 @@ struct orc_model {
     uint32_t seed;     /* lazy: the synthetic weights' seed and mode */
     int wmode;
     int cur_layer;     /* lazy: layer whose weights the [0] buffers hold (-1: none) */
+    int threads;       /* orc_model_set_threads: GEMV rows over this many host threads (default 1) */
 };
 
 /* ---- synthetic weight generation over host threads (test-infrastructure speed only: every element is a
@@ -310,6 +311,7 @@ static orc_model* model_create(const orc_config* cfg, int lazy) {
     int KV = m->kv_dim;
     m->lazy = lazy;
     m->cur_layer = -1;
+    m->threads = 1;
     int LW = lazy ? 1 : L; /* lazy: one buffer set, regenerated layer by layer */
     m->emb = (float*)calloc((size_t)V * D, sizeof(float));
     m->norm = alloc_tab(2 * L + 1, (size_t)D);
@@ -520,6 +522,39 @@ static double now_s(void) {
     return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
 }
 
+/* The CPU baseline's secondary "all host cores, not reference" line: a GEMV's rows split over
+ * threads. Every row is still one sequential fp32 sum, so the results are bit-identical to orc_matmul. */
+typedef struct {
+    const float *x, *w;
+    float* y;
+    int r0, r1, cols;
+} mm_job;
+static void* mm_worker(void* p) {
+    mm_job* j = (mm_job*)p;
+    orc_matmul(j->x, j->w + (size_t)j->r0 * j->cols, j->y + j->r0, j->r1 - j->r0, j->cols, 1.0f);
+    return NULL;
+}
+static void mm(const orc_model* m, const float* x, const float* w, float* y, int rows, int cols) {
+    int nt = m->threads > 32 ? 32 : m->threads;
+    if (nt <= 1 || rows < 2 * nt) {
+        orc_matmul(x, w, y, rows, cols, 1.0f);
+        return;
+    }
+    pthread_t th[32];
+    mm_job jobs[32];
+    for (int t = 0; t < nt; t++) {
+        jobs[t] = (mm_job){x, w, y, (int)((int64_t)rows * t / nt), (int)((int64_t)rows * (t + 1) / nt), cols};
+        if (pthread_create(&th[t], NULL, mm_worker, &jobs[t]) != 0) {
+            mm_worker(&jobs[t]);
+            th[t] = 0;
+        }
+    }
+    for (int t = 0; t < nt; t++)
+        if (th[t]) pthread_join(th[t], NULL);
+}
+
+void orc_model_set_threads(orc_model* m, int n) { m->threads = n < 1 ? 1 : n; }
+
 /* source/model/model.cpp:40-140 */
 int orc_model_forward(orc_model* m, int token, int pos, float* logits_out) {
     const orc_config* c = &m->c;
@@ -540,9 +575,9 @@ int orc_model_forward(orc_model* m, int token, int pos, float* logits_out) {
         orc_rmsnorm(m->x, m->norm[2 * l], m->h, D, c->eps);          /* :52 */
         float* krow = m->kcache + ((size_t)l * T + pos) * KV;        /* :54-55 slice_KV_cache */
         float* vrow = m->vcache + ((size_t)l * T + pos) * KV;
-        orc_matmul(m->h, m->wq[lw], m->q, D, D, 1.0f);                /* :58 */
-        orc_matmul(m->h, m->wk[lw], krow, KV, D, 1.0f);               /* :60 */
-        orc_matmul(m->h, m->wv[lw], vrow, KV, D, 1.0f);               /* :62 */
+        mm(m, m->h, m->wq[lw], m->q, D, D);                /* :58 */
+        mm(m, m->h, m->wk[lw], krow, KV, D);               /* :60 */
+        mm(m, m->h, m->wv[lw], vrow, KV, D);               /* :62 */
         orc_rope(m->q, krow, pos, m->sin_c, m->cos_c, D, KV, c->head_dim); /* :66-67 */
         if (m->kv_f16) {
             for (int j = 0; j < KV; j++) {
@@ -552,18 +587,18 @@ int orc_model_forward(orc_model* m, int token, int pos, float* logits_out) {
         }
         orc_mha(m->q, m->score, m->kcache, m->vcache, m->attn, l, pos, T, c->head_dim, c->n_heads,
                 c->n_kv_heads);                                       /* :70-78 */
-        orc_matmul(m->attn, m->wo[lw], m->o, D, D, 1.0f);             /* :80-83 */
+        mm(m, m->attn, m->wo[lw], m->o, D, D);             /* :80-83 */
         orc_add(m->x, m->o, m->x1, D);                               /* :86-90 */
         orc_rmsnorm(m->x1, m->norm[2 * l + 1], m->h, D, c->eps);     /* :93-96 */
-        orc_matmul(m->h, m->up[lw], m->u, I, D, 1.0f);                /* :99-102 */
-        orc_matmul(m->h, m->gate[lw], m->g, I, D, 1.0f);              /* :105-108 */
+        mm(m, m->h, m->up[lw], m->u, I, D);                /* :99-102 */
+        mm(m, m->h, m->gate[lw], m->g, I, D);              /* :105-108 */
         orc_swiglu(m->u, m->g, m->a, I);                             /* :111-115 */
-        orc_matmul(m->a, m->down[lw], m->f, D, I, 1.0f);              /* :118-121 */
+        mm(m, m->a, m->down[lw], m->f, D, I);              /* :118-121 */
         orc_add(m->f, m->x1, m->x, D);                               /* :124-128 */
     }
     double t2 = now_s();
     orc_rmsnorm(m->x, m->norm[2 * L], m->h, D, c->eps);              /* :131-134 */
-    orc_matmul(m->h, m->emb, logits_out, V, D, 1.0f);                /* :136-139 tied head */
+    mm(m, m->h, m->emb, logits_out, V, D);               /* :136-139 tied head */
     double t3 = now_s();
     m->t_embed = t1 - t0;
     m->t_layers = t2 - t1;

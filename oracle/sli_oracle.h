@@ -77,6 +77,9 @@ int orc_model_forward(orc_model* m, int token, int pos, float* logits_out);
  * token fed at position t; logits_out (optional) is [max_length][V]. */
 int orc_model_predict(orc_model* m, const int* prompt, int n_prompt, int max_length, int* tokens_out,
                       float* logits_out);
+/* GEMV rows of the forward split over n host threads (bit-identical results; the CPU baseline's secondary
+ * all-cores line, BASELINE.md §4 — not the reference, which is single-threaded). Default 1. */
+void orc_model_set_threads(orc_model* m, int n);
 /* seconds spent in the last forward: embedding, transformer layers, final norm + LM head. */
 void orc_model_last_timing(const orc_model* m, double* t_embed, double* t_layers, double* t_head);
 /* write the reference's flat fp32 weight file (model.cpp:336-469 order). */

@@ -1424,7 +1424,12 @@ static int get_state(sli_model* m, int seq, int32_t* pos, int32_t* token, int32_
 // The GEMM prefill (prefill.h) needs fp16 or int8 weights, batch 1, head_dim 64 or 128 and 64-multiple
 // projection depths; otherwise the prompt runs through the decode step itself (teacher forcing), which gives
 // the same tokens.
+// The chunked MFMA prefill (prefill.h) takes GEMM depths that are multiples of 64 (int8: 128-deep stages with a
+// half last stage). A multi-process TP rank without an RCCL communicator (SLI_DEBUG_NOCOMM, with or without the
+// one-shot exchange) has no all-reduce for a chunk's M x D residual rows, so it prefills through the decode step,
+// whose exchange it does have; an in-process group sums the chunk rows itself (record_group_prefill).
 static bool pf_supported(const sli_model* m) {
+    if (m->partial && !m->collectives && !m->group) return false;
     return m->c.w_dtype != SLI_DT_F32 && m->B == 1 && (m->hd == 64 || m->hd == 128) && m->D % 64 == 0 &&
            m->D <= 8192 && m->Il % 64 == 0 && (m->hq * m->hd) % 64 == 0;
 }
@@ -1461,6 +1466,8 @@ static std::vector<PfState> pf_chunks(int n) {
     for (int p0 = 0; p0 < n - 1; p0 += kPfMaxChunk) cs.push_back(PfState{p0, std::min(kPfMaxChunk, n - 1 - p0)});
     return cs;
 }
+
+extern "C" int sli_model_prefill_path(const sli_model* m) { return m && m->B == 1 && pf_supported(m) ? 1 : 0; }
 
 extern "C" int sli_model_prefill(sli_model* m, const int32_t* ids, int32_t n) {
     SLI_CHECK(m && ids, SLI_ERR_ARG, "null argument");

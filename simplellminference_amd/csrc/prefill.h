@@ -213,7 +213,11 @@ __global__ void __launch_bounds__(128 * Cfg::WR) pgemm_kernel(PgIn<WT> in, Epi e
     const int rb = (slot / PB) * 8 + xcd, pb = slot - (slot / PB) * PB;
     const int nrb = (in.N + Geo::BN - 1) / Geo::BN;
     if (rb >= nrb) return;  // (uniform) padding of the grid to a multiple of 8 row blocks
-    const int ns = in.K / Geo::KS;  // stages
+    // stages: K is a multiple of 64, so with int8 weights (KS 128) the last stage may be a half stage. Its DMA
+    // pieces past the row's end reload the stage's first half instead (in bounds; never read), and only its
+    // first KBS / 2 k-blocks are multiplied.
+    const int ns = (in.K + Geo::KS - 1) / Geo::KS;
+    const bool half_tail = (in.K % Geo::KS) != 0;
     const int nt = in.N >> 4;       // row tiles
     const unsigned ring = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)pg_smem;
 
@@ -221,7 +225,8 @@ __global__ void __launch_bounds__(128 * Cfg::WR) pgemm_kernel(PgIn<WT> in, Epi e
     // lands at byte 16 i of it: image row i / cpr, physical chunk i % cpr (cpr = 16-B chunks per image row),
     // so it loads the row's logical chunk (i % cpr) ^ swizzle(row).
     const char* src[Geo::DPW];
-    int adv[Geo::DPW];  // bytes per stage
+    int adv[Geo::DPW];   // bytes per stage
+    int back[Geo::DPW];  // bytes to step back in a half last stage (logical chunk in the stage's second half)
 #pragma unroll
     for (int j = 0; j < Geo::DPW; ++j) {
         const int off = (wave * Geo::DPW + j) * 1024;
@@ -232,6 +237,7 @@ __global__ void __launch_bounds__(128 * Cfg::WR) pgemm_kernel(PgIn<WT> in, Epi e
             const int row = epi.row(min(t, nt - 1), r);
             src[j] = reinterpret_cast<const char*>(in.W) + (size_t)row * in.K * sizeof(WT) + c * 16;
             adv[j] = Geo::A_ROW;
+            back[j] = c >= 4 ? Geo::A_ROW / 2 : 0;
         } else {
             constexpr int cpr = Geo::B_ROW / 16;
             const int o2 = off - Geo::A_BYTES;
@@ -242,13 +248,15 @@ __global__ void __launch_bounds__(128 * Cfg::WR) pgemm_kernel(PgIn<WT> in, Epi e
             const int m = pb * BM + pt * 16 + r;
             src[j] = reinterpret_cast<const char*>(B) + (size_t)m * in.K * 2 + c * 16;
             adv[j] = Geo::B_ROW;
+            back[j] = c >= cpr / 2 ? Geo::B_ROW / 2 : 0;
         }
     }
     auto issue = [&](int s) {
         const unsigned dst = ring + (unsigned)((s % S) * Geo::STAGE);
+        const bool tail = half_tail && s == ns - 1;
 #pragma unroll
         for (int j = 0; j < Geo::DPW; ++j)
-            pf_dma(src[j] + (size_t)s * adv[j], dst + (unsigned)((wave * Geo::DPW + j) * 1024));
+            pf_dma(src[j] + (size_t)s * adv[j] - (tail ? back[j] : 0), dst + (unsigned)((wave * Geo::DPW + j) * 1024));
     };
 
     pf_float4 acc[2][Geo::WPT];
@@ -267,8 +275,10 @@ __global__ void __launch_bounds__(128 * Cfg::WR) pgemm_kernel(PgIn<WT> in, Epi e
         __builtin_amdgcn_s_barrier();  // every wave's pieces of s landed; every wave is done with s - 1
         if (s + S - 1 < ns) issue(s + S - 1);  // into the buffer of s - 1
         const char* st = pg_smem + (size_t)(s % S) * Geo::STAGE;
+        const int kbs = (half_tail && s == ns - 1) ? KBS / 2 : KBS;  // wave-uniform
 #pragma unroll
         for (int kb = 0; kb < KBS; ++kb) {
+            if (kb >= kbs) break;
             u32x4 af[2], bh[Geo::WPT], bl[Geo::WPT];
 #pragma unroll
             for (int a = 0; a < 2; ++a) {

@@ -234,6 +234,10 @@ class LlamaModel:
         p = np.ascontiguousarray(prompt_ids, np.int32)
         call("sli_model_prefill", self._h, p.ctypes.data_as(ctypes.c_void_p), p.size)
 
+    def prefill_path(self) -> str:
+        """'mfma' (chunked MFMA GEMMs) or 'decode' (teacher-forced decode steps): sli_model_prefill_path."""
+        return "mfma" if _lib.load().sli_model_prefill_path(self._h) == 1 else "decode"
+
     def predict_prefill(self, prompt_ids, max_length: int, want_logits: bool = False):
         """predict() with the prompt prefilled; logits rows of positions < len(prompt) - 1 are NaN."""
         p = np.ascontiguousarray(prompt_ids, np.int32)

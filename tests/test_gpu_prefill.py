@@ -127,9 +127,26 @@ def test_prefill_int8(gpu, oracle, kv, n):
     _check(gtok, glog, otok, olog, n)
 
 
+@pytest.mark.parametrize("over", [dict(intermediate_size=704), dict(hidden_size=320, num_attention_heads=5,
+                                                                      num_key_value_heads=5, kv_hidden_size=320)])
+def test_prefill_int8_half_last_stage(gpu, oracle, over):
+    """int8 GEMM depths that are 64 mod 128 (the int8 pgemm stage is 128 deep): the last stage is a half stage
+    (prefill.h). Llama-2-7B int8 at TP 4 has such a down projection (2752 = 21.5 x 128); here the FFN width
+    704 (down) and a hidden size of 320 (q/k/v, gate/up and wo)."""
+    cfg, om, gm = _pair(oracle, "tiny", w="i8", kv="f16", max_length=160, **over)
+    assert gm.prefill_path() == "mfma"
+    prompt = _prompt(150, cfg.vocab_size)
+    otok, olog = om.predict(prompt, 160)
+    gtok, glog = gm.predict_prefill(prompt, 160, want_logits=True)
+    gm.close()
+    om.close()
+    _check(gtok, glog, otok, olog, 150)
+
+
 def test_prefill_f32_weights_teacher_forces(gpu, oracle):
     """fp32 weights have no MFMA projection: the prompt runs through the decode step (same tokens)."""
     cfg, om, gm = _pair(oracle, "tiny-gqa", w="f32", kv="f32")
+    assert gm.prefill_path() == "decode"
     prompt = _prompt(13, cfg.vocab_size)
     otok, olog = om.predict(prompt, 30)
     gtok, glog = gm.predict_prefill(prompt, 30, want_logits=True)
@@ -162,12 +179,15 @@ def test_prefill_twice_reuses_graphs(gpu, oracle):
     om.close()
 
 
-@pytest.mark.parametrize("name,tp,w", [("tiny-h8", 2, "f16"), ("tiny-h8", 8, "f16"), ("tiny-gqa-h16", 4, "i8")])
-def test_prefill_tp_group(gpu, oracle, name, tp, w):
+@pytest.mark.parametrize("name,tp,w,over", [("tiny-h8", 2, "f16", {}), ("tiny-h8", 8, "f16", {}),
+                                            ("tiny-gqa-h16", 4, "i8", {}),
+                                            ("tiny-gqa-h16", 4, "i8", dict(intermediate_size=2816))])
+def test_prefill_tp_group(gpu, oracle, name, tp, w, over):
     """The sharded prefill (sli_tp_group_prefill): every rank's chunk GEMMs on its shard, the residual rows
-    summed over the ranks after every wo and down GEMM; against the unsharded oracle."""
+    summed over the ranks after every wo and down GEMM; against the unsharded oracle. FFN 2816 at TP 4: each
+    rank's int8 down projection is 704 deep, a half last stage (the Llama-2-7B int8 TP-4 case)."""
     from simplellminference_amd.model import TPGroup, preset
-    cfg = preset(name, max_length=160)
+    cfg = preset(name, max_length=160, **over)
     g = TPGroup(cfg, tp, w_dtype=w, kv_dtype="f16", seed=2).init()
     om = oracle.Model(_ocfg(oracle, cfg), seed=2, wmode=_wmode(oracle, w), kv_f16=True)
     prompt = _prompt(140, cfg.vocab_size)

@@ -130,7 +130,10 @@ def test_tp_rank_of_c2_shapes_steps_nocomm(gpu, monkeypatch, w, world):
     m.close()
 
 
-def _oneshot_rank(rank, world, port, name, batch, q, mode="oneshot", w="f16"):
+LONG_PROMPT = [(7 * i + 3) % 500 for i in range(23)]
+
+
+def _oneshot_rank(rank, world, port, name, batch, q, mode="oneshot", w="f16", prefill=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0",
                       SLI_DEBUG_NOCOMM="1")  # no RCCL communicator: the one-shot kernels are the only exchange
     import torch
@@ -146,7 +149,10 @@ def _oneshot_rank(rank, world, port, name, batch, q, mode="oneshot", w="f16"):
         tp.open_oneshot(m)
         m.set_allreduce(mode)
         dist.barrier()
-        if batch == 1:
+        if prefill:
+            path = m.prefill_path()
+            toks, logits = m.predict_prefill(LONG_PROMPT, 32, want_logits=True)
+        elif batch == 1:
             toks, logits = m.predict(PROMPT, 16, want_logits=True)
         else:
             toks, logits = m.predict_batch([PROMPT, [5, 6, 7]][:batch], 16, want_logits=True)
@@ -156,7 +162,7 @@ def _oneshot_rank(rank, world, port, name, batch, q, mode="oneshot", w="f16"):
         dist.barrier()
         m.close()
         if rank == 0:
-            q.put(("ok", toks, np.concatenate([p.numpy() for p in parts], axis=-1), err))
+            q.put(("ok", toks, np.concatenate([p.numpy() for p in parts], axis=-1), err if not prefill else (err, path)))
     except Exception as e:  # report to the parent instead of hanging it
         q.put(("err", repr(e), None, None))
     dist.destroy_process_group()
@@ -190,6 +196,36 @@ def test_oneshot_allreduce_two_processes(gpu, name, batch, mode):
     assert err == 0
     assert np.array_equal(toks, rtoks)
     assert np.abs(logits - rlogits).max() <= 1e-3
+
+
+@pytest.mark.parametrize("mode", ["oneshot", "fused"])
+def test_oneshot_prefill_two_processes(gpu, mode):
+    """Prompt prefill on two rank processes whose only exchange is the one-shot all-reduce (no RCCL
+    communicator): the chunked prefill has no exchange for a chunk's residual rows, so the engine takes the
+    teacher-forced decode path (sli_model_prefill_path == 0), whose one-shot exchange it does have; tokens equal
+    the TP = 1 engine's prefilled predict, logits within 1e-3 (prefill used to copy the unreduced
+    partials there)."""
+    from simplellminference_amd.model import LlamaModel, preset
+    ref = LlamaModel(config=preset("tiny-gqa"), w_dtype="f16", kv_dtype="f16", seed=0).init()
+    assert ref.prefill_path() == "mfma"
+    rtoks, rlogits = ref.predict_prefill(LONG_PROMPT, 32, want_logits=True)
+    ref.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_oneshot_rank, args=(r, 2, port, "tiny-gqa", 1, q, mode, "f16", True))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    status, toks, logits, info = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+    assert status == "ok", toks
+    err, path = info
+    assert err == 0 and path == "decode"
+    assert np.array_equal(toks, rtoks)
+    n = len(LONG_PROMPT)
+    assert np.abs(logits[n - 1:] - rlogits[n - 1:]).max() <= 1e-3
 
 
 @pytest.mark.parametrize("name,world,mode,w", [("tiny-h8", 4, "fused", "f16"), ("tiny-h8", 4, "oneshot", "f16"),
