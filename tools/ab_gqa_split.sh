@@ -1,5 +1,5 @@
 #!/bin/bash
-# GQA-4 attention as two GQA-2 groups per kv head (SLI_ATTN_GQA_SPLIT=1): parity, then A/B at C4 and Llama-3-8B B1
+# SLI_ATTN_GQA_SPLIT=2|4 (a GQA-4 kv head as two GQA-2 groups or four MHA heads): parity, then A/B at C4 and Llama-3-8B B1
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 SLI_ATTN_GQA_SPLIT=2 timeout -k 10 400 python -u -m pytest tests/test_gpu_batch.py -x -q --timeout 300 --timeout-method thread > gpurun_out/gs_tests2.log 2>&1 || { tail -30 gpurun_out/gs_tests2.log; exit 1; }

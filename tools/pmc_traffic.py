@@ -17,12 +17,17 @@ from collections import defaultdict
 path, alg, out, key = sys.argv[1], float(sys.argv[2]), sys.argv[3], sys.argv[4]
 dom = sys.argv[5] if len(sys.argv) > 5 else None  # the bench line's dominant family (whose bytes alg are)
 per = defaultdict(list)
+rows = []  # (dispatch id, kernel, value) in dispatch order
 for r in csv.DictReader(open(path)):
     if r.get("Counter_Name") != "FETCH_SIZE":
         continue
     per[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    rows.append((int(r.get("Dispatch_Id") or len(rows)), r["Kernel_Name"], float(r["Counter_Value"])))
+rows.sort()
+
+
 def weight_kernel(k):  # the step's weight-streaming kernels: batch-1 GEMV or the batched MFMA projection
-    return "gemv_kernel" in k or "gemv_merge_kernel" in k or "bgemm_kernel" in k
+    return "gemv_kernel" in k or "gemv_merge_kernel" in k or "gemv_sum_kernel" in k or "bgemm_kernel" in k
 
 
 gemv = [v for k, vs in per.items() if weight_kernel(k) for v in vs]
@@ -55,20 +60,24 @@ def family(k):
     for tag, fam in (("EpiQKV", "qkv"), ("EpiSwiGLU", "gate_up"), ("EpiLogits", "lm_head")):
         if tag in k and weight_kernel(k):
             return fam
-    if "gemv_merge_kernel" in k:  # wo: its input staged from the attention's split partials
+    if "gemv_merge_kernel" in k:  # wo: its input staged from the attention's split partials (EpiKPart: K-split)
         return "wo"
-    if "gemv_kernel" in k and "EpiStore<1>" in k:  # the only other single-row residual GEMV of a step
+    if "gemv_kernel" in k and ("EpiStore<1>" in k or "EpiStoreSum<1" in k):  # the other single-row residual GEMV
         return "down"
     if "bgemm_kernel" in k and "BgEpiStore" in k:
-        return "wo+down"  # one instantiation serves both batched row-parallel projections
+        return "wo|down"  # one instantiation serves both batched row-parallel projections: split by order below
     return None
 
 
 fam = defaultdict(list)
-for k, vs in per.items():
+nth = 0  # batched row-parallel projections alternate wo, down in a step's dispatch order (engine record_phase)
+for _, k, v in rows:
     f = family(k)
+    if f == "wo|down":
+        f = "wo" if nth % 2 == 0 else "down"
+        nth += 1
     if f:
-        fam[f] += vs
+        fam[f].append(v)
 res[key]["per_family_hbm_bytes_per_launch"] = {f: round(2 * 1024 * sum(v) / len(v)) for f, v in fam.items()}
 if dom in res[key]["per_family_hbm_bytes_per_launch"]:
     res[key]["dominant_family_hbm_over_algorithmic"] = round(res[key]["per_family_hbm_bytes_per_launch"][dom] / alg, 4)
