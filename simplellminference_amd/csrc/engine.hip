@@ -72,6 +72,8 @@ struct sli_model {
     float *x = nullptr, *xpart = nullptr, *q = nullptr, *attn = nullptr, *act = nullptr, *logits = nullptr;
     float* part = nullptr;
     unsigned* attn_count = nullptr;
+    int wo_ks = 1;              // batch-1 TP-1 wo split over its columns (wo_ksplit): partials [wo_ks][D]
+    float* wo_part = nullptr;
     float *sin_t = nullptr, *cos_t = nullptr;
     unsigned long long* keys = nullptr;
     sli::DevState* st = nullptr;
@@ -527,6 +529,7 @@ struct StepRecorder {
     // (attention launched with defer_merge, gemv.h XStageMerge)
     static int gemv_wo(sli_model* m, int l) {
         const LayerW& w = m->layers[l];
+        if (m->wo_ks > 1) return gemv_wo_ks(m, l);
         const bool tp = m->partial;
         GemvIn in{m->attn, nullptr, 0.0f, m->hq * m->hd};
         EpiStore<1> e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, w.wo_s, 1.0f, m->D};
@@ -548,6 +551,24 @@ struct StepRecorder {
             SLI_HIP((launch_gemv_merge<WT, 1, UW, NT>((const WT*)w.wo, in, e, am, m->D, m->stream)));
         return SLI_OK;
     }
+    // wo split over its columns (wo_ksplit): part[k][d] = wo[d][k-th column block] . attn[k-th block]
+    static int gemv_wo_ks(sli_model* m, int l) {
+        const LayerW& w = m->layers[l];
+        const int ks = m->wo_ks;
+        GemvIn in{m->attn, nullptr, 0.0f, m->hq * m->hd / ks};
+        const EpiKPart e{m->wo_part, w.wo_s, m->D, ks};
+        AttnMergeIn am{m->part, &m->st->pos, attn_max_splits(m), attn_wg_positions(m->c.kv_dtype, m->hd), m->hd};
+        am.ksplit = ks;
+        am.kunits = m->D;
+        const int grid = gemv_ksplit_grid(m->D, ks);
+        // a row block is QD / ks columns: 128 fp16 / 64 int8 16-byte vectors, one chunk of U per lane
+        constexpr int UK = std::is_same<WT, int8_t>::value ? 1 : 2;
+        if (am.max_splits > 8)
+            SLI_HIP((launch_gemv_merge_ks<WT, 1, UK, NT, EpiKPart, 16>((const WT*)w.wo, in, e, am, grid, m->stream)));
+        else
+            SLI_HIP((launch_gemv_merge_ks<WT, 1, UK, NT, EpiKPart>((const WT*)w.wo, in, e, am, grid, m->stream)));
+        return SLI_OK;
+    }
     static int attn_max_splits(sli_model* m) {
         const int ppwg = attn_wg_positions(m->c.kv_dtype, m->hd);
         return (m->T + ppwg - 1) / ppwg;
@@ -556,6 +577,14 @@ struct StepRecorder {
         const LayerW& w = m->layers[l];
         GemvIn in{m->x, m->norms + (size_t)(2 * l + 1) * m->D, m->c.eps, m->D};
         EpiSwiGLU e{m->act, w.gu_s, m->Il, m->c.act_mode};
+        if (m->wo_ks > 1) {  // stage x1 = x + the K-split wo's partials (XStageSum)
+            constexpr int UG = std::is_same<WT, int8_t>::value ? 2 : 4;  // launch_gemv_u's unsplit U
+            if (m->wo_ks == 2)
+                SLI_HIP((launch_gemv_sum<WT, 2, UG, NT, EpiSwiGLU, 2>((const WT*)w.gu, in, e, m->wo_part, m->Il, m->stream)));
+            else
+                SLI_HIP((launch_gemv_sum<WT, 2, UG, NT, EpiSwiGLU, 4>((const WT*)w.gu, in, e, m->wo_part, m->Il, m->stream)));
+            return SLI_OK;
+        }
         SLI_HIP((launch_gemv_u<WT, 2, 4, NT>((const WT*)w.gu, in, e, m->Il, m->stream)));
         return SLI_OK;
     }
@@ -571,8 +600,20 @@ struct StepRecorder {
                 SLI_HIP((launch_gemv_u<WT, 1, 6, NT>((const WT*)w.down, in, ep, m->D, m->stream)));
             return SLI_OK;
         }
+        if (m->wo_ks == 2) return gemv_down_sum<2>(m, w, in);
+        if (m->wo_ks == 4) return gemv_down_sum<4>(m, w, in);
         EpiStore<1> e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, w.down_s, 1.0f, m->D};
         if constexpr (std::is_same<WT, int8_t>::value)  // tools/gemv_lab i8: R1U4 11.66 us vs R1U3 11.74
+            SLI_HIP((launch_gemv<WT, 1, 4, NT>((const WT*)w.down, in, e, m->D, m->stream)));
+        else
+            SLI_HIP((launch_gemv_u<WT, 1, 6, NT>((const WT*)w.down, in, e, m->D, m->stream)));
+        return SLI_OK;
+    }
+    // down + residual x1 = x + the K-split wo's partials (EpiStoreSum: XStageSum's order), written to x
+    template <int NP>
+    static int gemv_down_sum(sli_model* m, const LayerW& w, const GemvIn& in) {
+        const EpiStoreSum<1, NP> e{m->x, m->x, m->wo_part, w.down_s, m->D};
+        if constexpr (std::is_same<WT, int8_t>::value)
             SLI_HIP((launch_gemv<WT, 1, 4, NT>((const WT*)w.down, in, e, m->D, m->stream)));
         else
             SLI_HIP((launch_gemv_u<WT, 1, 6, NT>((const WT*)w.down, in, e, m->D, m->stream)));
@@ -1111,6 +1152,23 @@ int sli_comm_get_id(void* out) {
 }
 
 // group != null: rank cfg->tp_rank of an in-process group (shares the group's stream, no communicator)
+// The batch-1 wo GEMV split over its input columns (gemv.h EpiKPart): ks workgroup blocks, block k streams columns
+// [k QD / ks, (k + 1) QD / ks) of every row and merges only those heads' attention split partials, so a workgroup
+// stages 1/ks of the 32 heads x 8 splits it reads unsplit (C1: 133 KB per workgroup, as many bytes as its weight
+// rows at int8). The ks partial row sums go to wo_part; the gate/up GEMV stages x + sum(parts) (XStageSum) and
+// the down GEMV's residual is the same sum (EpiStoreSum). Batch 1, TP 1 (a TP rank's wo feeds the exchange),
+// D <= 4096 (XStageSum's one round). SLI_WO_KSPLIT=1 / 2 / 4 (A/B).
+static int wo_ksplit(const sli_model* m) {
+    const char* e = getenv("SLI_WO_KSPLIT");  // read per model (tests switch it between models)
+    const int env = e ? atoi(e) : 1;
+    const int ks = env == 2 || env == 4 ? env : 1;
+    if (ks == 1 || m->B != 1 || m->partial || m->group || m->D > 4 * sli::kGemvThreads || m->hq % ks) return 1;
+    const int cols = m->hq * m->hd / ks;
+    const int epv = 16 / (int)m->wbytes;  // weight elements per 16-byte vector
+    if (cols % epv || cols % 4 || sli::gemv_ksplit_grid(m->D, ks) == 0) return 1;
+    return ks;
+}
+
 static int create_model(const sli_model_config* cfg, const void* comm_id, sli_tp_group* group, sli_model** out) {
     SLI_CHECK(cfg && out, SLI_ERR_ARG, "sli_model_create: null");
     const sli_model_config& c = *cfg;
@@ -1267,6 +1325,8 @@ static int create_model(const sli_model_config* cfg, const void* comm_id, sli_tp
         ncclResult_t r = ncclCommInitRank(&m->comm, c.tp_size, id, c.tp_rank);
         if (r != ncclSuccess) return bail(fail(SLI_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r)));
     }
+    m->wo_ks = wo_ksplit(m);
+    if (m->wo_ks > 1 && (rc = model_alloc(m, (void**)&m->wo_part, sizeof(float) * m->wo_ks * D)) != SLI_OK) return bail(rc);
     *out = m;
     return SLI_OK;
 }

@@ -122,6 +122,10 @@ struct AttnMergeIn {
     const float* part;       // [heads][max_splits][hd + kAttnPartPad]
     const int32_t* pos_dev;  // the live context: ns = min(pos / ppwg + 1, max_splits)
     int max_splits, ppwg, hd;
+    // K-split wo (EpiKPart): the launch's units are ksplit blocks of kunits (k-major), a workgroup's units all lie
+    // in one block k, and it stages (merges) only the heads of input quarter k: in.cols / hd heads from head
+    // k * in.cols / hd on. ksplit 1: the whole input.
+    int ksplit = 1, kunits = 0;
 };
 
 template <int G, int NS = 8>
@@ -130,11 +134,17 @@ struct XStageMerge {
     float4 ov[NS];
     float2 ml[NS];
     int pos = 0;
+    int h0 = 0;  // first head of this workgroup's input (K-split wo)
     __device__ __forceinline__ const float* row(int f, int s) const {
-        const int h = f / (am.hd >> 2);
+        const int h = h0 + f / (am.hd >> 2);
         return am.part + ((size_t)h * am.max_splits + min(s, am.max_splits - 1)) * (am.hd + kAttnPartPad);
     }
     __device__ __forceinline__ void issue(const GemvIn& in) {
+        if (am.ksplit > 1) {  // the block k of the workgroup's first unit (gemv_block's balanced partition)
+            const int nw = kGemvThreads >> 6;
+            const int ub = (int)(((unsigned)(blockIdx.x * nw) * (unsigned)(am.ksplit * am.kunits)) / (unsigned)(gridDim.x * nw));
+            h0 = (ub / am.kunits) * (in.cols / am.hd);
+        }
         const int f = min((int)threadIdx.x, (in.cols >> 2) - 1);  // the first round of the input
         const int d4 = f % (am.hd >> 2);
         pos = *am.pos_dev;
@@ -191,6 +201,64 @@ struct XStageMerge {
         const int ns = min(pos / am.ppwg + 1, am.max_splits);
         if ((int)threadIdx.x < n4) xs4[xswz<G>(threadIdx.x)] = merge_regs(threadIdx.x, ns);
         for (int f = threadIdx.x + kGemvThreads; f < n4; f += kGemvThreads) xs4[xswz<G>(f)] = merge_mem(f, ns);
+    }
+};
+
+// The input x + p_0 + ... + p_{NP-1} (the K-split wo's partial row sums, EpiKPart, added in that order), then
+// optionally RMS-normalised like XStage (rms_kernel.cpp:5-23): the gate/up GEMV of a layer whose wo ran K-split
+// stages the residual stream x1 = x + wo . attn (model.cpp:86-90) itself. One round only: cols <= 4 *
+// kGemvThreads (the host checks), so every input float4 and its partials are one thread's registers (a thread
+// past the input repeats the last float4 with the same value).
+template <int G, int NP>
+struct XStageSum {
+    const float* parts;  // [NP][cols]
+    float4 xr, wr, pr[NP];
+    __device__ __forceinline__ void issue(const GemvIn& in) {
+        const int f = min((int)threadIdx.x, (in.cols >> 2) - 1);
+        xr = reinterpret_cast<const float4*>(in.x)[f];
+        wr = reinterpret_cast<const float4*>(in.norm_w ? in.norm_w : in.x)[f];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) pr[k] = reinterpret_cast<const float4*>(parts + (size_t)k * in.cols)[f];
+    }
+    __device__ __forceinline__ void commit(float* smem, const GemvIn& in) {
+        float* red = smem;
+        float4* xs4 = reinterpret_cast<float4*>(smem + kGemvLdsHead);
+        const int tid = threadIdx.x, n4 = in.cols >> 2, f = min(tid, n4 - 1);
+        float4 v = xr;
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            v.x += pr[k].x;
+            v.y += pr[k].y;
+            v.z += pr[k].z;
+            v.w += pr[k].w;
+        }
+        if (in.norm_w == nullptr) {
+            xs4[xswz<G>(f)] = v;
+            return;
+        }
+        const float m = tid < n4 ? 1.0f : 0.0f;
+        float ss = m * (v.x * v.x);
+        ss += m * (v.y * v.y);
+        ss += m * (v.z * v.z);
+        ss += m * (v.w * v.w);
+        ss = wave_sum(ss);
+        if ((tid & 63) == 0) red[tid >> 6] = ss;
+        __syncthreads();
+        if (tid == 0) {
+            float t = 0.0f;
+            for (int w = 0; w < (kGemvThreads >> 6); ++w) t += red[w];
+            const float tep = t / (float)in.cols;  // rms_kernel.cpp:17
+            const float rms = sqrtf(tep + in.eps);  // :18
+            red[32] = 1.0f / rms;                   // :19
+        }
+        __syncthreads();
+        const float inv = red[32];
+        float4 o;  // :20-22  y = (x * inv) * w
+        o.x = (v.x * inv) * wr.x;
+        o.y = (v.y * inv) * wr.y;
+        o.z = (v.z * inv) * wr.z;
+        o.w = (v.w * inv) * wr.w;
+        xs4[xswz<G>(f)] = o;
     }
 };
 
@@ -440,6 +508,16 @@ __global__ void __launch_bounds__(kGemvThreads) gemv_merge_kernel(const WT* __re
     gemv_block<WT, R, U, NT, Epi, XStageMerge<Vec16<WT>::N / 4, NS>, NB>(W, in, epi, stage, smem);
 }
 
+// a GEMV whose input is x plus NP partial vectors (XStageSum)
+template <typename WT, int R, int U, bool NT, class Epi, int NP, int NB = 2>
+__global__ void __launch_bounds__(kGemvThreads) gemv_sum_kernel(const WT* __restrict__ W, GemvIn in, Epi epi_in,
+                                                                const float* parts) {
+    Epi epi = epi_in;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    XStageSum<Vec16<WT>::N / 4, NP> stage{parts};
+    gemv_block<WT, R, U, NT, Epi, XStageSum<Vec16<WT>::N / 4, NP>, NB>(W, in, epi, stage, smem);
+}
+
 // Row-by-row fallback for shapes the vector kernel cannot take (cols*sizeof(WT) not a multiple of 16
 // or a misaligned base): one wave per row, scalar loads. Only the op-level API reaches it.
 template <typename WT>
@@ -502,6 +580,82 @@ struct EpiStore {
                 y[row] = resid ? (pre ? pre_r[i] : resid[row]) + a : a;
             }
         }
+    }
+    __device__ void finish(float*) const {}
+};
+
+// EpiStore whose residual is x + p_0 + ... + p_{NP-1} (the K-split wo's partials, summed in XStageSum's order,
+// so the residual is bit-identical to the x1 the gate/up GEMV normalised): y[row] = x1[row] + sum * rscale[row].
+template <int R, int NP>
+struct EpiStoreSum {
+    float* y;
+    const float* resid;  // x
+    const float* parts;  // [NP][nrows]
+    const float* rscale;
+    int nrows;
+    int pre_u = -1;
+    float pre_r[R] = {}, pre_s[R] = {};
+    __device__ int units() const { return (nrows + R - 1) / R; }
+    __device__ void rows(int u, int* r) const {
+#pragma unroll
+        for (int i = 0; i < R; ++i) r[i] = min(u * R + i, nrows - 1);
+    }
+    __device__ float x1(int row) const {
+        float v = resid[row];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) v += parts[(size_t)k * nrows + row];
+        return v;
+    }
+    __device__ void prefetch_a(int u) {
+        pre_u = u;
+        const float* sp = rscale ? rscale : resid;
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const int row = min(u * R + i, nrows - 1);
+            pre_r[i] = x1(row);
+            pre_s[i] = sp[row];
+        }
+    }
+    __device__ void prefetch_b(int) {}
+    __device__ void store(int u, const int*, const float* v) const {
+        const bool pre = u == pre_u;
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const int row = u * R + i;
+            if (row < nrows) {
+                const float a = rscale ? v[i] * (pre ? pre_s[i] : rscale[row]) : v[i];
+                y[row] = (pre ? pre_r[i] : x1(row)) + a;
+            }
+        }
+    }
+    __device__ void finish(float*) const {}
+};
+
+// K-split wo (model.cpp:80-83 without the residual add): the [D][QD] weight read as a [D * ks][QD / ks] matrix
+// (row d * ks + k = columns [k QD / ks, (k + 1) QD / ks) of row d, the same bytes), unit u = (k = u / D, d = u % D)
+// so a workgroup's units share one k; part[k][d] = (row sum) * rscale[d]. The residual add moves to the consumers
+// (XStageSum, EpiStoreSum).
+struct EpiKPart {
+    float* part;  // [ks][D]
+    const float* rscale;
+    int D, ks;
+    int pre_u = -1;
+    float pre_s = 1.0f;
+    __device__ int units() const { return D * ks; }
+    __device__ void rows(int u, int* r) const {
+        const int k = u / D;
+        r[0] = (u - k * D) * ks + k;
+    }
+    __device__ void prefetch_a(int u) {
+        pre_u = u;
+        const int k = u / D;
+        pre_s = rscale ? rscale[u - k * D] : 1.0f;
+    }
+    __device__ void prefetch_b(int) {}
+    __device__ void store(int u, const int*, const float* v) const {
+        const int k = u / D;
+        const float s = rscale ? (u == pre_u ? pre_s : rscale[u - k * D]) : 1.0f;
+        part[u] = v[0] * s;
     }
     __device__ void finish(float*) const {}
 };
@@ -747,6 +901,39 @@ hipError_t launch_gemv_merge(const WT* W, const GemvIn& in_, const Epi& epi, con
     const size_t lds = gemv_lds_bytes(in.cols) + sizeof(float) * gemv_res_floats(units, grid, R);
     hipLaunchKernelGGL((gemv_merge_kernel<WT, R, U, NT, Epi, NS, NB>), dim3(grid), dim3(kGemvThreads), lds, s, W, in,
                        epi, am);
+    return hipGetLastError();
+}
+
+// K-split wo: the grid must keep every workgroup's units inside one block k (gemv_block's partition b * N / g):
+// g = ks * m with m dividing D, so each workgroup holds D / m units of one k. 0 if no such grid fits the chip.
+inline int gemv_ksplit_grid(int D, int ks) {
+    const int maxb = gemv_max_blocks();
+    for (int m = maxb / ks; m >= 1; --m)
+        if (D % m == 0) return ks * m;
+    return 0;
+}
+template <typename WT, int R, int U, bool NT, class Epi, int NS = 8, int NB = SLI_WO_NB>
+hipError_t launch_gemv_merge_ks(const WT* W, const GemvIn& in_, const Epi& epi, const AttnMergeIn& am, int grid,
+                                hipStream_t s) {
+    const int units = am.ksplit * am.kunits;
+    if (in_.csplit != 1 || grid <= 0 || grid % am.ksplit || am.kunits % (grid / am.ksplit)) return hipErrorInvalidValue;
+    GemvIn in = in_;
+    in.cw = gemv_wave_count<WT>(units, grid);
+    const size_t lds = gemv_lds_bytes(in.cols) + sizeof(float) * gemv_res_floats(units, grid, R);
+    hipLaunchKernelGGL((gemv_merge_kernel<WT, R, U, NT, Epi, NS, NB>), dim3(grid), dim3(kGemvThreads), lds, s, W, in,
+                       epi, am);
+    return hipGetLastError();
+}
+template <typename WT, int R, int U, bool NT, class Epi, int NP, int NB = 2>
+hipError_t launch_gemv_sum(const WT* W, const GemvIn& in_, const Epi& epi, const float* parts, int units,
+                           hipStream_t s) {
+    if (in_.csplit != 1 || in_.cols > 4 * kGemvThreads) return hipErrorInvalidValue;  // XStageSum: one round
+    GemvIn in = in_;
+    const int grid = gemv_balanced_blocks(units);
+    in.cw = gemv_wave_count<WT>(units, grid);
+    const size_t lds = gemv_lds_bytes(in.cols) + sizeof(float) * gemv_res_floats(units, grid, R);
+    hipLaunchKernelGGL((gemv_sum_kernel<WT, R, U, NT, Epi, NP, NB>), dim3(grid), dim3(kGemvThreads), lds, s, W, in,
+                       epi, parts);
     return hipGetLastError();
 }
 
