@@ -13,9 +13,13 @@
 //      vmcnt and a raw s_barrier (cdna_hip_programming.md §5 "Pipelining across barriers"). Fused epilogues:
 //      RoPE + K/V cache rows + q (model.cpp:52-67), residual add (:86-90, :124-128), SwiGLU (:111-115,
 //      written straight as the down projection's hi/lo operand);
-//   3. pf_attn_kernel: block-causal attention of a 64-position query block of one head against the cache
-//      rows 0 .. position (mha_kernel.cpp:36-77 per query: s_t = q.k_t * scale, softmax, sum p_t v_t), fp32,
-//      K/V tiles of 64 positions in LDS, online softmax.
+//   3. pf_attn_mfma_kernel (fp16 KV, the default): block-causal attention of 16 chunk rows x one head against
+//      the cache rows 0 .. position (mha_kernel.cpp:36-77 per query: s_t = q.k_t * scale, softmax, sum p_t v_t):
+//      S = K q^T on MFMA with q split hi/lo, online softmax in fp32, P V on MFMA with V read transposed
+//      (ds_read_b64_tr_b16) from LDS-DMA'd K/V tiles; pf_attn_kernel, the VALU form (fp32, 64-position query
+//      blocks, K/V tiles of 64 positions in LDS), serves fp32 KV caches.
+// int8 weights: stages of 128 k; a depth that is 64 mod 128 (e.g. Llama-2-7B int8 down at TP 4, 2752) ends with
+// a half stage (pgemm_kernel).
 // The chunk's start position and valid count live in device memory (PfState), so one captured graph per
 // chunk size serves every chunk of every prompt.
 #pragma once

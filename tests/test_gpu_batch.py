@@ -154,29 +154,38 @@ def test_llama3_8b_full_batch8_properties(gpu):
 def test_llama3_8b_full_batch8_matches_oracle(gpu, oracle):
     """The whole C4 workload at TP 1 (Llama-3-8B, 32 layers, vocab 128256, batch 8, ctx 4096) against the
     oracle's full forward per sequence (the lazy oracle: each layer's weights regenerated in turn), ragged
-    positions. Bar: the same argmax for every sequence and logits within 1e-3 relative to the largest logit
-    (north star: "1e-3 fp16 tolerance"). At contexts of 1-5 positions, 32 layers amplify the difference
-    between two valid fp32 summation orders (the oracle's sequential sums vs the GPU's tree sums) to
-    1.0-1.5e-3 absolute on logits of |5.7| — 2.6e-4 relative — in the batch-1 GEMV path and the batched MFMA
-    path alike (tools/diag_c4_pos1.py, profiles/r3_full_model_parity.txt); longer contexts stay below 3e-4."""
+    positions. Bar: the same argmax for every sequence and logits within 1e-3 absolute (north star: "1e-3 fp16
+    tolerance"). Sequence 5 sits at position 1, where 32 layers amplify the oracle's sequential fp32 sums: a
+    float64 restatement of that step (tests/golden/make_f64_c4.py, committed as c4_f64_seq5.npz) puts the ORACLE
+    1.33e-3 from float64, so that sequence is bounded against the float64 logits instead (1e-3 absolute) and
+    against the oracle by 1e-3 plus the oracle's own measured error."""
+    import os
     from simplellminference_amd.model import LlamaModel, preset
+    f64 = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c4_f64_seq5.npz"))
     cfg = preset("llama3-8b")
     gm = LlamaModel(config=cfg, w_dtype="f16", kv_dtype="f16", seed=1, batch=8).init()
     gm.fill_kv_synthetic(7, 4095)
     tokens = [1234 + 9001 * b for b in range(8)]
     positions = [4095, 4095, 100, 2047, 4000, 1, 3333, 4095]
+    assert (tokens[5], positions[5], 7 + 5) == (int(f64["token"]), int(f64["pos"]), int(f64["kv_seed"]))
     got = gm.forward_batch(tokens, positions)
     gm.close()
+    err64 = float(np.abs(got[5] - f64["logits"]).max())
+    print(f"C4 sequence 5 (pos 1): GPU vs float64 max|d| {err64:.2e}; oracle vs float64 {float(f64['oracle_err']):.2e}")
+    assert err64 <= 1e-3, err64
+    assert int(np.argmax(got[5])) == int(f64["argmax"])
     om = oracle.Model(_ocfg(oracle, cfg), seed=1, wmode=oracle.W_F16, kv_f16=True, lazy=True)
     errs = []
     for b in range(8):
         om.fill_kv_synthetic(7 + b, 4095)
         want = om.forward(tokens[b], positions[b])
-        errs.append(float(np.abs(got[b] - want).max() / max(1.0, float(np.abs(want).max()))))
+        errs.append(float(np.abs(got[b] - want).max()))
         assert int(np.argmax(got[b])) == int(np.argmax(want)), b
     om.close()
-    print(f"C4 full model, per-sequence max|dlogit| / max|logit|: {['%.2e' % e for e in errs]}")
-    assert max(errs) <= 1e-3, errs
+    print(f"C4 full model, per-sequence max|dlogit| vs the oracle: {['%.2e' % e for e in errs]}")
+    bound = [1e-3] * 8
+    bound[5] = 1e-3 + float(f64["oracle_err"])
+    assert all(e <= b for e, b in zip(errs, bound)), errs
 
 
 @pytest.mark.parametrize("world", [2, 8])
