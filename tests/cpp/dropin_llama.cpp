@@ -85,7 +85,7 @@ int main(int argc, char** argv) {
     auto mha = std::make_shared<op::MultiHeadAttention>(dev, T, hd, cfg.num_attention_heads, cfg.num_key_value_heads);
     auto add = std::make_shared<op::VecAddLayer>(dev, D);
     auto swiglu = std::make_shared<op::SwigluLayer>(dev, I);
-    op::argmaxLayer argmax(dev, V);
+    op::argmaxLayer argmax(DeviceType::kDeviceCPU, V);  // host argmax, as model.cpp create_nonparam_layers makes it
 
     auto da = mem::CUDADeviceAllocatorFactory::get_instance();
     auto ca = mem::CPUDeviceAllocatorFactory::get_instance();
@@ -127,14 +127,14 @@ int main(int argc, char** argv) {
         }
         norms[2 * L]->forward(x, h);
         cls->forward(h, logits);
-        std::vector<float> host(V);
-        da->memcpy(logits.ptr<float>(), host.data(), 4 * (size_t)V, base::MemcpyKind::kMemcpyCUDA2CPU);
-        log1.insert(log1.end(), host.begin(), host.end());
+        mem::Tensor pred_cpu({V}, true, ca);  // model.cpp:175-179: logits to the host, then the host argmax
+        ca->memcpy(logits.ptr<float>(), pred_cpu.ptr<float>(), 4 * (size_t)V, base::MemcpyKind::kMemcpyCUDA2CPU);
+        log1.insert(log1.end(), pred_cpu.ptr<float>(), pred_cpu.ptr<float>() + V);
         if (pos < (int)prompt.size() - 1) {
             input_token.index<int32_t>(0) = prompt[++pos];
         } else {
             ++pos;
-            argmax.forward(logits, input_token);  // device argmax -> host token
+            argmax.forward(pred_cpu, input_token);
         }
         position.index<int32_t>(0) = pos;
     }
