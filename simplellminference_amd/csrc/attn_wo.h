@@ -38,6 +38,8 @@ struct AttnWoArgs {
     int D, QD, ks;
     int heads_per_k;            // q heads per column block: hq / ks
     int group_wgs;              // arrivals per head group per launch: (hkv / ks) * max_splits
+    int dbg = 0;                // SLI_DEBUG_AW bits (diagnosis): 1 weights after the publish, 2 x_k -> dbg_x
+    float* dbg_x = nullptr;     // [ks][QD / ks] merged inputs (dbg & 2)
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t aw_rsrc(const void* p, unsigned bytes) {
@@ -77,9 +79,10 @@ __global__ void __launch_bounds__(kAwThreads) attn_wo_kernel(AttnArgs<KT> a, Att
         }
     };
     bool issued = false;
+    const bool late = (w.dbg & 1) != 0;
     auto pre = [&]() {
-        if (wave >= SW) issue();
-        issued = true;
+        if (wave >= SW && !late) issue();
+        issued = !late;
     };
     a.defer_merge = 3;
     attn_publish<KT, HD, G, 16, attn_late_v(G)>(a, kvh, split, pre);
@@ -145,6 +148,8 @@ __global__ void __launch_bounds__(kAwThreads) attn_wo_kernel(AttnArgs<KT> a, Att
             }
         }
         reinterpret_cast<float4*>(aw_x)[f] = make_float4(o.x / L, o.y / L, o.z / L, o.w / L);
+        if ((w.dbg & 2) && (blockIdx.x % (gridDim.x / w.ks)) == 0)
+            reinterpret_cast<float4*>(w.dbg_x + (size_t)k * C)[f] = make_float4(o.x / L, o.y / L, o.z / L, o.w / L);
     }
     __syncthreads();
 

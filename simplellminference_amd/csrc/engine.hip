@@ -584,6 +584,10 @@ struct StepRecorder {
             const int ks = m->wo_ks;
             AttnWoArgs<WT> aw{(const WT*)w.wo, w.wo_s, m->wo_part, m->aw_cnt, &m->st->error, m->D, m->hq * m->hd, ks,
                               m->hq / ks, (m->hkv / ks) * splits};
+            if (const char* e = getenv("SLI_DEBUG_AW")) {  // diagnosis only: see AttnWoArgs::dbg
+                aw.dbg = atoi(e);
+                aw.dbg_x = m->attn;  // the merged attention output lands where the unfused op path writes it
+            }
             const size_t lds = sizeof(float) * (size_t)(m->hq * m->hd / ks);
             hipLaunchKernelGGL((attn_wo_kernel<KT, WT, HD_, G_, RW_, NVL_>), dim3(m->hkv * splits), dim3(kAwThreads), lds,
                                m->stream, a, aw);
