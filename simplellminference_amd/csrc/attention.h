@@ -210,7 +210,7 @@ __device__ __forceinline__ bool attn_publish(const AttnArgs<KT>& a, int kvh, int
         }
     }
     __syncthreads();
-    if (a.defer_merge) {  // partials for the next launch (the kernel boundary publishes them): plain stores
+    if (a.defer_merge == 1 || a.defer_merge == 2) {  // partials for the next launch (the kernel boundary publishes them): plain stores
         for (int i = threadIdx.x; i < G * HD; i += 64 * WAVES) {
             const int g = i / HD, d = i - g * HD;
             float M = -INFINITY;
