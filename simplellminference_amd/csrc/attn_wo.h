@@ -38,7 +38,8 @@ struct AttnWoArgs {
     int D, QD, ks;
     int heads_per_k;            // q heads per column block: hq / ks
     int group_wgs;              // arrivals per head group per launch: (hkv / ks) * max_splits
-    int dbg = 0;                // SLI_DEBUG_AW bits (diagnosis): 1 weights after the publish, 2 x_k -> dbg_x
+    int dbg = 0;                // SLI_DEBUG_AW bits (diagnosis): 1 weights after the publish, 2 x_k -> dbg_x,
+                                // timing only (wrong results): 4 no wait, 8 no merge loads
     float* dbg_x = nullptr;     // [ks][QD / ks] merged inputs (dbg & 2)
 };
 
@@ -95,7 +96,7 @@ __global__ void __launch_bounds__(kAwThreads) attn_wo_kernel(AttnArgs<KT> a, Att
         const unsigned long long old = __hip_atomic_fetch_add(w.cnt + g_att, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long target = (old / (unsigned long long)w.group_wgs + 1ull) * (unsigned long long)w.group_wgs;
         int ok = 1;
-        for (unsigned spins = 0; __hip_atomic_load(w.cnt + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++spins) {
+        for (unsigned spins = 0; !(w.dbg & 4) && __hip_atomic_load(w.cnt + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++spins) {
             __builtin_amdgcn_s_sleep(1);
             if (spins > (1u << 22)) {
                 __hip_atomic_fetch_or(w.err, kAwErrTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -113,7 +114,7 @@ __global__ void __launch_bounds__(kAwThreads) attn_wo_kernel(AttnArgs<KT> a, Att
     const int ns = min(pos / AttnGeom<KT, HD>::PPWG + 1, a.max_splits);
     const int h0 = k * w.heads_per_k;
     const auto rs = aw_rsrc(a.part, (unsigned)(sizeof(float) * (size_t)(h0 + w.heads_per_k) * a.max_splits * PS));
-    const int n4 = C >> 2;
+    const int n4 = (w.dbg & 8) ? 0 : C >> 2;
     for (int f = threadIdx.x; f < n4; f += kAwThreads) {
         const int h = h0 + f / (HD / 4), d4 = f - (f / (HD / 4)) * (HD / 4);
         const unsigned row0 = (unsigned)(h * a.max_splits) * PS;
