@@ -41,15 +41,7 @@ struct AttnArgs {
                             // narrower groups that share each K/V row through the L2, ops.hip mha_launch_hd)
     int defer_merge = 0;    // != 0: only write the workgroup partials (plain stores); the splits are merged
                             // after the launch: 1 by the consumer (the wo GEMV's input staging, gemv.h
-                            // XStageMerge), 2 by attn_merge_kernel (mha_launch launches it); 3: published
-                            // write-through (sc1) and drained, no arrival counter (the fused attention + wo
-                            // launch counts its own arrivals, attn_wo.h)
-};
-
-// attn_publish's hook for work whose loads go out right behind the K/V and q loads (attn_wo.h issues the wo
-// weight rows there): called once per wave, by every wave, before the scores
-struct AttnNoPre {
-    __device__ __forceinline__ void operator()() {}
+                            // XStageMerge), 2 by attn_merge_kernel (mha_launch launches it)
 };
 
 // Position of the sequence that owns (batched) kv head kvh.
@@ -102,8 +94,8 @@ __host__ __device__ constexpr bool attn_late_v(int g) { return g == 1 ? SLI_ATTN
 // The split work of workgroup (kvh, wgs): partial state published write-through, arrival counted.
 // Returns true in the head's last-arriving workgroup (which must then merge the head: attn_merge).
 // Every return is uniform over the workgroup.
-template <typename KT, int HD, int G, int WAVES = attn_waves(G), bool LATE_V = attn_late_v(G), class Pre = AttnNoPre>
-__device__ __forceinline__ bool attn_publish(const AttnArgs<KT>& a, int kvh, int wgs, Pre pre = Pre{}) {
+template <typename KT, int HD, int G, int WAVES = attn_waves(G), bool LATE_V = attn_late_v(G)>
+__device__ __forceinline__ bool attn_publish(const AttnArgs<KT>& a, int kvh, int wgs) {
     using Geo = AttnGeom<KT, HD>;
     constexpr int kAttnNit = kAttnSlots / WAVES;
     constexpr int EPV = Geo::EPV, LPR = Geo::LPR, RPI = Geo::RPI, PPW = kAttnNit * RPI;
@@ -152,9 +144,6 @@ __device__ __forceinline__ bool attn_publish(const AttnArgs<KT>& a, int kvh, int
         for (int g = 0; g < G; ++g)
 #pragma unroll
             for (int e = 0; e < EPV; ++e) qv[g][e] = a.q[(size_t)(kvh * G + g) * HD + li * EPV + e];
-        __builtin_amdgcn_sched_barrier(0);
-        pre();  // behind every load the scores wait for (vmcnt counts in issue order)
-        __builtin_amdgcn_sched_barrier(0);
         float s[kAttnNit][G];
 #pragma unroll
         for (int it = 0; it < kAttnNit; ++it) {
@@ -194,8 +183,6 @@ __device__ __forceinline__ bool attn_publish(const AttnArgs<KT>& a, int kvh, int
 #pragma unroll
             for (int e = 0; e < EPV; ++e) ov[g][e] = stride_sum<LPR>(ov[g][e]);
         }
-    } else {
-        pre();
     }
     if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 4 + 1] = __builtin_amdgcn_s_memrealtime();
     if (sub == 0) {
@@ -210,7 +197,7 @@ __device__ __forceinline__ bool attn_publish(const AttnArgs<KT>& a, int kvh, int
         }
     }
     __syncthreads();
-    if (a.defer_merge == 1 || a.defer_merge == 2) {  // partials for the next launch (the kernel boundary publishes them): plain stores
+    if (a.defer_merge) {  // partials for the next launch (the kernel boundary publishes them): plain stores
         for (int i = threadIdx.x; i < G * HD; i += 64 * WAVES) {
             const int g = i / HD, d = i - g * HD;
             float M = -INFINITY;
@@ -255,11 +242,8 @@ __device__ __forceinline__ bool attn_publish(const AttnArgs<KT>& a, int kvh, int
             __hip_atomic_store(dst + HD + 1, L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    // every storing wave drains before the arrival (waves with no partial store skip it: a wave of the fused
-    // attention + wo launch may have wo weight loads in flight that the arrival must not wait for)
-    if ((int)threadIdx.x < ((G * HD + 63) / 64) * 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before the arrival
     __syncthreads();
-    if (a.defer_merge == 3) return false;  // the caller counts the arrival (attn_wo.h)
     const int ns = min(pos / (WAVES * PPW) + 1, a.max_splits);  // live workgroups of this kv head
     if (threadIdx.x == 0) {
         const unsigned prev = __hip_atomic_fetch_add(a.counters + kvh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -25,7 +25,6 @@
 
 #include "../../include/sli_synth.h"
 #include "attention.h"
-#include "attn_wo.h"
 #include "bgemm.h"
 #include "common.h"
 #include "gemv.h"
@@ -75,8 +74,6 @@ struct sli_model {
     unsigned* attn_count = nullptr;
     int wo_ks = 1;              // batch-1 TP-1 wo split over its columns (wo_ksplit): partials [wo_ks][D]
     float* wo_part = nullptr;
-    int aw_rw = 0;              // > 0: attention + K-split wo as one launch (attn_wo.h), aw_rw wo rows per wave
-    unsigned long long* aw_cnt = nullptr;  // its per-head-group arrival counters [wo_ks], monotonic
     float *sin_t = nullptr, *cos_t = nullptr;
     unsigned long long* keys = nullptr;
     sli::DevState* st = nullptr;
@@ -572,38 +569,6 @@ struct StepRecorder {
             SLI_HIP((launch_gemv_merge_ks<WT, 1, UK, NT, EpiKPart>((const WT*)w.wo, in, e, am, grid, m->stream)));
         return SLI_OK;
     }
-    // attention + K-split wo as one launch (attn_wo.h)
-    template <int HD_, int G_, int RW_, int NVL_>
-    static int attn_wo_go(sli_model* m, int l) {
-        if constexpr (std::is_same<KT, __half>::value && !std::is_same<WT, float>::value) {
-            const int splits = attn_max_splits(m);
-            const long long hs = (long long)m->T * m->hd, ls = (long long)m->hkv * hs;
-            AttnArgs<KT> a{m->q, (const KT*)m->kc + l * ls, (const KT*)m->vc + l * ls, m->hd, hs, m->part, nullptr,
-                           nullptr, &m->st->pos, 0, m->hkv, splits, 1.0f / sqrtf((float)HD_), m->hkv, 0};
-            const LayerW& w = m->layers[l];
-            const int ks = m->wo_ks;
-            AttnWoArgs<WT> aw{(const WT*)w.wo, w.wo_s, m->wo_part, m->aw_cnt, &m->st->error, m->D, m->hq * m->hd, ks,
-                              m->hq / ks, (m->hkv / ks) * splits};
-            if (const char* e = getenv("SLI_DEBUG_AW")) {  // diagnosis only: see AttnWoArgs::dbg
-                aw.dbg = atoi(e);
-                aw.dbg_x = m->attn;  // the merged attention output lands where the unfused op path writes it
-            }
-            const size_t lds = sizeof(float) * (size_t)(m->hq * m->hd / ks);
-            hipLaunchKernelGGL((attn_wo_kernel<KT, WT, HD_, G_, RW_, NVL_>), dim3(m->hkv * splits), dim3(kAwThreads), lds,
-                               m->stream, a, aw);
-            SLI_HIP(hipGetLastError());
-            return SLI_OK;
-        } else {
-            return fail(SLI_ERR_STATE, "attn_wo: fp16 K/V, fp16 or int8 weights");
-        }
-    }
-    static int attn_wo(sli_model* m, int l) {
-        const bool g2 = m->hq == 2 * m->hkv;
-        constexpr bool I8 = std::is_same<WT, int8_t>::value;
-        constexpr int N4 = I8 ? 1 : 2, N2 = I8 ? 2 : 4;  // vectors per lane at 4 / 2 rows per wave
-        if (m->aw_rw == 4) return g2 ? attn_wo_go<128, 2, 4, N4>(m, l) : attn_wo_go<128, 1, 4, N4>(m, l);
-        return g2 ? attn_wo_go<128, 2, 2, N2>(m, l) : attn_wo_go<128, 1, 2, N2>(m, l);
-    }
     static int attn_max_splits(sli_model* m) {
         const int ppwg = attn_wg_positions(m->c.kv_dtype, m->hd);
         return (m->T + ppwg - 1) / ppwg;
@@ -797,7 +762,6 @@ struct StepRecorder {
             const long long ps = m->hd, hs = (long long)m->T * m->hd;
             const long long ls = (long long)m->B * m->hkv * m->T * m->hd;
             SLI_TRY(batched ? b_qkv(m, l) : gemv_qkv(m, l));
-            if (m->aw_rw > 0) return attn_wo(m, l);  // attention + wo as one launch (attn_wo.h)
             // a batch is B * hkv kv heads of one layer: sequence b owns kv heads [b*hkv, (b+1)*hkv)
             SLI_TRY(mha_launch<KT>(m->q, (const KT*)m->kc, (const KT*)m->vc, m->attn, l, 0, &m->st->pos, m->T, m->hd,
                                    m->B * m->hq, m->B * m->hkv, ps, hs, ls, m->part, m->attn_count, s,
@@ -1053,10 +1017,6 @@ struct StepRecorder {
             switch (f) {
                 case SLI_FAM_QKV: SLI_TRY(batched ? b_qkv(m, l) : gemv_qkv(m, l)); break;
                 case SLI_FAM_ATTN: {
-                    if (m->aw_rw > 0) {  // the fused attention + wo launch
-                        SLI_TRY(attn_wo(m, l));
-                        break;
-                    }
                     const long long ps = m->hd, hs = (long long)m->T * m->hd;
                     const long long ls = (long long)m->B * m->hkv * m->T * m->hd;
                     SLI_TRY(mha_launch<KT>(m->q, (const KT*)m->kc, (const KT*)m->vc, m->attn, l, 0, &m->st->pos, m->T,
@@ -1065,10 +1025,7 @@ struct StepRecorder {
                                            batched ? defer_batched() : 1));
                     break;
                 }
-                case SLI_FAM_WO:
-                    if (m->aw_rw > 0) break;  // inside the attention family's launch
-                    SLI_TRY(batched ? b_wo(m, l) : gemv_wo(m, l));
-                    break;
+                case SLI_FAM_WO: SLI_TRY(batched ? b_wo(m, l) : gemv_wo(m, l)); break;
                 case SLI_FAM_GU: SLI_TRY(batched ? b_gu(m, l) : gemv_gu(m, l)); break;
                 case SLI_FAM_DOWN: SLI_TRY(batched ? b_down(m, l) : gemv_down(m, l)); break;
                 default: return fail(SLI_ERR_ARG, "unknown kernel family");
@@ -1211,30 +1168,6 @@ static int wo_ksplit(const sli_model* m) {
     const int epv = 16 / (int)m->wbytes;  // weight elements per 16-byte vector
     if (cols % epv || cols % 4 || sli::gemv_ksplit_grid(m->D, ks) == 0) return 1;
     return ks;
-}
-
-// The fused attention + K-split wo launch (attn_wo.h; SLI_ATTN_WO=1): wo rows per wave, or 0 where it does not
-// apply. Needs the K-split wo, fp16 K/V at head_dim 128, 16-wave attention workgroups (MHA / GQA-2) whose grid
-// (kv heads x context splits) fits the chip at one workgroup per CU (every wait's producers resident), that grid
-// being a K-split wo grid (gemv_ksplit_grid's condition), whole kv heads per column block, and a register
-// shape the kernel is instantiated for (fp16: 4 rows x 2 vectors or 2 x 4; int8: 4 x 1 or 2 x 2).
-static int attn_wo_rows(const sli_model* m) {
-    const char* e = getenv("SLI_ATTN_WO");
-    if (!(e && e[0] == '1') || m->wo_ks < 2 || m->c.kv_dtype != SLI_DT_F16 || m->hd != 128) return 0;
-    if (m->c.w_dtype != SLI_DT_F16 && m->c.w_dtype != SLI_DT_I8) return 0;
-    const int g = m->hq / m->hkv;
-    if (g != 1 && g != 2) return 0;
-    const int ks = m->wo_ks, ppwg = attn_wg_positions(m->c.kv_dtype, m->hd);
-    const int grid = m->hkv * ((m->T + ppwg - 1) / ppwg);
-    if (grid > device_cus() || grid % ks || m->hkv % ks || (ks * m->D) % (grid * 16)) return 0;
-    const int upw = ks * m->D / grid, rw = upw / 16;
-    if (m->D % (grid / ks) || (m->hq / ks) % g) return 0;
-    const int nvl = (m->hq * m->hd / ks) * (int)m->wbytes / 16 / 64;
-    if ((m->hq * m->hd / ks) * (int)m->wbytes % (16 * 64)) return 0;
-    const bool f16 = m->c.w_dtype == SLI_DT_F16;
-    if (f16 ? !((rw == 4 && nvl == 2) || (rw == 2 && nvl == 4)) : !((rw == 4 && nvl == 1) || (rw == 2 && nvl == 2)))
-        return 0;
-    return rw;
 }
 
 static int create_model(const sli_model_config* cfg, const void* comm_id, sli_tp_group* group, sli_model** out) {
@@ -1395,11 +1328,6 @@ static int create_model(const sli_model_config* cfg, const void* comm_id, sli_tp
     }
     m->wo_ks = wo_ksplit(m);
     if (m->wo_ks > 1 && (rc = model_alloc(m, (void**)&m->wo_part, sizeof(float) * m->wo_ks * D)) != SLI_OK) return bail(rc);
-    m->aw_rw = attn_wo_rows(m);
-    if (m->aw_rw > 0) {
-        if ((rc = model_alloc(m, (void**)&m->aw_cnt, sizeof(unsigned long long) * m->wo_ks)) != SLI_OK) return bail(rc);
-        if (hipMemset(m->aw_cnt, 0, sizeof(unsigned long long) * m->wo_ks) != hipSuccess) return bail(fail(SLI_ERR_HIP, "memset"));
-    }
     *out = m;
     return SLI_OK;
 }
@@ -2061,13 +1989,9 @@ int sli_model_time_families(sli_model* m, int32_t iters, double* us, double* byt
     bytes[SLI_FAM_GU] = 2.0 * m->Il * (D * wb + i8);
     bytes[SLI_FAM_DOWN] = D * (m->Il * wb + i8);
     bytes[SLI_FAM_LM] = (double)m->v_n * (D * wb + i8);
-    if (m->aw_rw > 0) {  // the attention family's launch carries wo (attn_wo.h): its bytes, no wo launches
-        bytes[SLI_FAM_ATTN] += bytes[SLI_FAM_WO];
-        bytes[SLI_FAM_WO] = 0.0;
-    }
     int rc = SLI_OK;
     for (int f = 0; rc == SLI_OK && f < SLI_FAM_COUNT; ++f) {
-        launches[f] = f == SLI_FAM_LM ? 1 : (f == SLI_FAM_WO && m->aw_rw > 0) ? 0 : m->L;
+        launches[f] = f == SLI_FAM_LM ? 1 : m->L;
         rc = SLI_DISPATCH(m, family, m, f);  // warm-up
         if (rc == SLI_OK && hipEventRecord(g.e0, m->stream) != hipSuccess) rc = fail(SLI_ERR_HIP, "event");
         for (int i = 0; rc == SLI_OK && i < iters; ++i) rc = SLI_DISPATCH(m, family, m, f);
@@ -2076,7 +2000,7 @@ int sli_model_time_families(sli_model* m, int32_t iters, double* us, double* byt
         if (rc == SLI_OK &&
             (hipEventSynchronize(g.e1) != hipSuccess || hipEventElapsedTime(&ms, g.e0, g.e1) != hipSuccess))
             rc = fail(SLI_ERR_HIP, "event timing");
-        us[f] = launches[f] ? 1000.0 * ms / ((double)iters * launches[f]) : 0.0;
+        us[f] = 1000.0 * ms / ((double)iters * launches[f]);
     }
     if (hipMemcpyAsync(m->x, g.xsave, xb, hipMemcpyDeviceToDevice, m->stream) != hipSuccess ||
         hipStreamSynchronize(m->stream) != hipSuccess) {
@@ -2138,10 +2062,6 @@ int sli_model_time_stream(sli_model* m, int32_t iters, double* us) {
                 a = (const char*)m->kc + l * kvl;
                 b = (const char*)m->vc + l * kvl;
                 na = nb = kvl;
-                if (m->aw_rw > 0) {  // the fused attention + wo launch also streams wo
-                    c = (const char*)w.wo;
-                    nc = D * m->hq * hd * wb;
-                }
                 break;
             case SLI_FAM_WO: a = (const char*)w.wo; na = D * m->hq * hd * wb; break;
             case SLI_FAM_GU: a = (const char*)w.gu; na = 2LL * m->Il * D * wb; break;
@@ -2152,10 +2072,6 @@ int sli_model_time_stream(sli_model* m, int32_t iters, double* us) {
     };
     for (int f = 0; f < SLI_FAM_COUNT; ++f) {
         const int n = f == SLI_FAM_LM ? 1 : m->L;
-        if (f == SLI_FAM_WO && m->aw_rw > 0) {  // no wo launches of its own
-            us[f] = 0.0;
-            continue;
-        }
         for (int l = 0; l < n; ++l) launch(f, l);  // warm-up
         SLI_HIP(hipEventRecord(g.e0, m->stream));
         for (int i = 0; i < iters; ++i)

@@ -307,9 +307,8 @@ class LlamaModel:
         n = len(self.FAMILIES)
         us, b, k = (ctypes.c_double * n)(), (ctypes.c_double * n)(), (ctypes.c_int32 * n)()
         call("sli_model_time_families", self._h, iters, us, b, k)
-        # a family with no launches of its own (wo inside the fused attention + wo launch) is left out
         return {f: {"avg_us": us[i], "bytes_per_launch": b[i], "launches_per_step": k[i]}
-                for i, f in enumerate(self.FAMILIES) if k[i] > 0}
+                for i, f in enumerate(self.FAMILIES)}
 
     def time_stream(self, iters: int = 20) -> dict:
         """Per kernel family: mean device µs of a pure streaming read of the same buffers (the floor)."""

@@ -80,55 +80,3 @@ def test_wo_ksplit_greedy_and_prefill(gpu, oracle, monkeypatch, ks):
     gm.close()
     om.close()
 
-
-# ---- attention + K-split wo as ONE launch (attn_wo.h; SLI_ATTN_WO=1) ---------------------------------------
-@pytest.mark.parametrize("ks", ["2", "4"])
-@pytest.mark.parametrize("w", ["f16", "i8"])
-def test_llama7b_two_layers_attn_wo(gpu, oracle, monkeypatch, ks, w):
-    """Llama-2-7B shapes at ctx 2048 (32 heads x 8 splits = 256 workgroups, one per CU): the fused launch is
-    active (no wo family of its own), the step at position 2047 matches the oracle, and a greedy run from
-    position 0 (one live split: the other workgroups only arrive) matches the unfused engine's tokens."""
-    monkeypatch.setenv("SLI_WO_KSPLIT", ks)
-    monkeypatch.setenv("SLI_ATTN_WO", "1")
-    om, gm = _models(oracle, "llama2-7b", w, "f16", seed=1, num_hidden_layers=2)
-    assert "wo" not in gm.time_families(2)
-    om.fill_kv_synthetic(7, 2047)
-    gm.fill_kv_synthetic(7, 2047)
-    want = om.forward(1234, 2047)
-    got = gm.forward(1234, 2047)
-    assert np.abs(got - want).max() <= 1e-3
-    assert int(np.argmax(got)) == int(np.argmax(want))
-    assert gm.state()["error"] == 0
-    gtok, glog = gm.predict(PROMPT, 24, want_logits=True)
-    assert gm.state()["error"] == 0
-    gm.close()
-    monkeypatch.setenv("SLI_ATTN_WO", "0")
-    from simplellminference_amd.model import LlamaModel, preset
-    ref = LlamaModel(config=preset("llama2-7b", num_hidden_layers=2), w_dtype=w, kv_dtype="f16", seed=1).init()
-    rtok, rlog = ref.predict(PROMPT, 24, want_logits=True)
-    ref.close()
-    om.close()
-    assert np.array_equal(gtok, rtok)
-    assert np.abs(glog - rlog).max() <= 1e-3
-
-
-def test_attn_wo_full_model_matches_oracle(gpu, oracle, monkeypatch):
-    """The C1 workload (32 layers, full vocab) with the fused launch, against the lazy oracle."""
-    monkeypatch.setenv("SLI_ATTN_WO", "1")
-    from simplellminference_amd.model import LlamaModel, preset
-    cfg = preset("llama2-7b")
-    gm = LlamaModel(config=cfg, w_dtype="f16", kv_dtype="f16", seed=1).init()
-    assert "wo" not in gm.time_families(1)
-    gm.fill_kv_synthetic(7, 2047)
-    got = gm.forward(1234, 2047)
-    assert gm.state()["error"] == 0
-    gm.close()
-    om = oracle.Model(oracle.Config(cfg.vocab_size, cfg.hidden_size, cfg.num_attention_heads,
-                                    cfg.num_key_value_heads, cfg.head_dim, cfg.intermediate_size,
-                                    cfg.num_hidden_layers, cfg.max_length, cfg.rms_norm_eps, cfg.rope_theta),
-                      seed=1, wmode=oracle.W_F16, kv_f16=True, lazy=True)
-    om.fill_kv_synthetic(7, 2047)
-    want = om.forward(1234, 2047)
-    om.close()
-    assert np.abs(got - want).max() <= 1e-3
-    assert int(np.argmax(got)) == int(np.argmax(want))
