@@ -561,12 +561,15 @@ struct StepRecorder {
         am.ksplit = ks;
         am.kunits = m->D;
         const int grid = gemv_ksplit_grid(m->D, ks);
-        // a row block is QD / ks columns: 128 fp16 / 64 int8 16-byte vectors, one chunk of U per lane
-        constexpr int UK = std::is_same<WT, int8_t>::value ? 1 : 2;
+        // U vectors per lane per step; NB steps in flight while the merge staging runs: fp16 4 (every step of the
+        // wave's rows at C1: wo 9.42 -> 8.97 us, +0.4 % tok/s; 3 is slower, 9.66), int8 2 (4 measured no faster)
+        // (profiles/r4_wo_nb_ab.txt)
+        constexpr bool I8 = std::is_same<WT, int8_t>::value;
+        constexpr int UK = I8 ? 1 : 2, NBK = I8 ? 2 : 4;
         if (am.max_splits > 8)
-            SLI_HIP((launch_gemv_merge_ks<WT, 1, UK, NT, EpiKPart, 16>((const WT*)w.wo, in, e, am, grid, m->stream)));
+            SLI_HIP((launch_gemv_merge_ks<WT, 1, UK, NT, EpiKPart, 16, NBK>((const WT*)w.wo, in, e, am, grid, m->stream)));
         else
-            SLI_HIP((launch_gemv_merge_ks<WT, 1, UK, NT, EpiKPart>((const WT*)w.wo, in, e, am, grid, m->stream)));
+            SLI_HIP((launch_gemv_merge_ks<WT, 1, UK, NT, EpiKPart, 8, NBK>((const WT*)w.wo, in, e, am, grid, m->stream)));
         return SLI_OK;
     }
     static int attn_max_splits(sli_model* m) {
