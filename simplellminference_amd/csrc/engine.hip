@@ -1164,7 +1164,10 @@ int sli_comm_get_id(void* out) {
 // 8.32 -> 7.43 us, +0.6 % / +1.9 % tok/s; 4 is no faster).
 static int wo_ksplit(const sli_model* m) {
     const char* e = getenv("SLI_WO_KSPLIT");  // read per model (tests switch it between models)
-    const int env = e ? atoi(e) : 2;  // measured (profiles/r4_wo_ksplit_ab.txt): 2 best at C1 and C3
+    // measured (profiles/r4_wo_ksplit_ab.txt): 2 best at ctx 2048 (8 attention splits per head); past 8 splits
+    // every workgroup stages twice the partials per head, so 4 there (SLI_WO_KSPLIT forces one)
+    const int ppwg = attn_wg_positions(m->c.kv_dtype, m->hd);
+    const int env = e ? atoi(e) : ((m->T + ppwg - 1) / ppwg > 8 ? 4 : 2);
     const int ks = env == 2 || env == 4 ? env : 1;
     if (ks == 1 || m->B != 1 || m->partial || m->group || m->D > 4 * sli::kGemvThreads || m->hq % ks) return 1;
     const int cols = m->hq * m->hd / ks;
