@@ -72,6 +72,8 @@ struct sli_model {
     float *x = nullptr, *xpart = nullptr, *q = nullptr, *attn = nullptr, *act = nullptr, *logits = nullptr;
     float* part = nullptr;
     unsigned* attn_count = nullptr;
+    int wo_merge = 1;           // batch 1: 1 = the wo GEMV merges the attention's splits while staging its input,
+                                // 0 = the attention's last-arriving workgroup merges them (wo_merges)
     int wo_ks = 1;              // batch-1 TP-1 wo split over its columns (wo_ksplit): partials [wo_ks][D]
     float* wo_part = nullptr;
     float *sin_t = nullptr, *cos_t = nullptr;
@@ -531,6 +533,16 @@ struct StepRecorder {
         const LayerW& w = m->layers[l];
         if (m->wo_ks > 1) return gemv_wo_ks(m, l);
         const bool tp = m->partial;
+        if (!m->wo_merge) {  // the attention merged its splits into attn: a plain input
+            GemvIn in{m->attn, nullptr, 0.0f, m->hq * m->hd};
+            if (fused_ar(m)) {
+                SLI_HIP((launch_gemv_u<WT, 1, 2, NT>((const WT*)w.wo, in, push_epi(m, w.wo_s), m->D, m->stream)));
+                return SLI_OK;
+            }
+            EpiStore<1> e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, w.wo_s, 1.0f, m->D};
+            SLI_HIP((launch_gemv_u<WT, 1, 2, NT>((const WT*)w.wo, in, e, m->D, m->stream)));
+            return SLI_OK;
+        }
         GemvIn in{m->attn, nullptr, 0.0f, m->hq * m->hd};
         EpiStore<1> e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, w.wo_s, 1.0f, m->D};
         const AttnMergeIn am{m->part, &m->st->pos, attn_max_splits(m), attn_wg_positions(m->c.kv_dtype, m->hd), m->hd};
@@ -768,7 +780,7 @@ struct StepRecorder {
             // a batch is B * hkv kv heads of one layer: sequence b owns kv heads [b*hkv, (b+1)*hkv)
             SLI_TRY(mha_launch<KT>(m->q, (const KT*)m->kc, (const KT*)m->vc, m->attn, l, 0, &m->st->pos, m->T, m->hd,
                                    m->B * m->hq, m->B * m->hkv, ps, hs, ls, m->part, m->attn_count, s,
-                                   batched ? m->hkv : 0, batched ? kPosStride : 0, 0, batched ? defer_batched() : 1));
+                                   batched ? m->hkv : 0, batched ? kPosStride : 0, 0, batched ? defer_batched() : m->wo_merge));
             return batched ? b_wo(m, l) : gemv_wo(m, l);
         }
         SLI_TRY(batched ? b_gu(m, l) : gemv_gu(m, l));
@@ -1025,7 +1037,7 @@ struct StepRecorder {
                     SLI_TRY(mha_launch<KT>(m->q, (const KT*)m->kc, (const KT*)m->vc, m->attn, l, 0, &m->st->pos, m->T,
                                            m->hd, m->B * m->hq, m->B * m->hkv, ps, hs, ls, m->part, m->attn_count,
                                            m->stream, batched ? m->hkv : 0, batched ? kPosStride : 0, 0,
-                                           batched ? defer_batched() : 1));
+                                           batched ? defer_batched() : m->wo_merge));
                     break;
                 }
                 case SLI_FAM_WO: SLI_TRY(batched ? b_wo(m, l) : gemv_wo(m, l)); break;
@@ -1155,6 +1167,18 @@ int sli_comm_get_id(void* out) {
 }
 
 // group != null: rank cfg->tp_rank of an in-process group (shares the group's stream, no communicator)
+// Where the batch-1 attention's context splits are merged. Up to 8 splits per head the wo GEMV merges them
+// while it stages its input (gemv.h XStageMerge: no serial tail in the attention launch). Past 8 (ctx > 2048
+// at head_dim 128, fp16 K/V) the 16-split register batch spills (128 VGPRs + scratch) and wo took 17 us at
+// ctx 4096 against 9 at 2048, so there the attention's last-arriving workgroup merges and wo stages a plain
+// input. SLI_WO_MERGE=0|1 forces it (A/B, profiles/r4_wo_merge_ab.txt).
+static int wo_merges(const sli_model* m) {
+    const char* e = getenv("SLI_WO_MERGE");
+    if (e && (e[0] == '0' || e[0] == '1')) return e[0] - '0';
+    const int ppwg = attn_wg_positions(m->c.kv_dtype, m->hd);
+    return (m->T + ppwg - 1) / ppwg > 8 ? 0 : 1;
+}
+
 // The batch-1 wo GEMV split over its input columns (gemv.h EpiKPart): ks workgroup blocks, block k streams columns
 // [k QD / ks, (k + 1) QD / ks) of every row and merges only those heads' attention split partials, so a workgroup
 // stages 1/ks of the 32 heads x 8 splits it reads unsplit (C1: 133 KB per workgroup, as many bytes as its weight
@@ -1164,12 +1188,10 @@ int sli_comm_get_id(void* out) {
 // 8.32 -> 7.43 us, +0.6 % / +1.9 % tok/s; 4 is no faster).
 static int wo_ksplit(const sli_model* m) {
     const char* e = getenv("SLI_WO_KSPLIT");  // read per model (tests switch it between models)
-    // measured (profiles/r4_wo_ksplit_ab.txt): 2 best at ctx 2048 (8 attention splits per head); past 8 splits
-    // every workgroup stages twice the partials per head, so 4 there (SLI_WO_KSPLIT forces one)
-    const int ppwg = attn_wg_positions(m->c.kv_dtype, m->hd);
-    const int env = e ? atoi(e) : ((m->T + ppwg - 1) / ppwg > 8 ? 4 : 2);
+    const int env = e ? atoi(e) : 2;  // measured (profiles/r4_wo_ksplit_ab.txt): 2 best at C1 and C3
     const int ks = env == 2 || env == 4 ? env : 1;
     if (ks == 1 || m->B != 1 || m->partial || m->group || m->D > 4 * sli::kGemvThreads || m->hq % ks) return 1;
+    if (!m->wo_merge) return 1;  // the split pays off in the merge staging it shrinks
     const int cols = m->hq * m->hd / ks;
     const int epv = 16 / (int)m->wbytes;  // weight elements per 16-byte vector
     if (cols % epv || cols % 4 || sli::gemv_ksplit_grid(m->D, ks) == 0) return 1;
@@ -1332,6 +1354,7 @@ static int create_model(const sli_model_config* cfg, const void* comm_id, sli_tp
         ncclResult_t r = ncclCommInitRank(&m->comm, c.tp_size, id, c.tp_rank);
         if (r != ncclSuccess) return bail(fail(SLI_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r)));
     }
+    m->wo_merge = m->B == 1 ? wo_merges(m) : 1;
     m->wo_ks = wo_ksplit(m);
     if (m->wo_ks > 1 && (rc = model_alloc(m, (void**)&m->wo_part, sizeof(float) * m->wo_ks * D)) != SLI_OK) return bail(rc);
     *out = m;

@@ -53,9 +53,12 @@ def test_llama7b_two_layers_wo_ksplit(gpu, oracle, monkeypatch, ks, w):
     assert int(np.argmax(got)) == int(np.argmax(want))
 
 
-@pytest.mark.parametrize("ks", ["2", "4"])
-def test_ctx4096_sixteen_splits_wo_ksplit(gpu, oracle, monkeypatch, ks):
-    """ctx 4096 (16 splits per head: the NS = 16 merge batch), GQA-4 Llama-3-8B shapes, 2 layers."""
+@pytest.mark.parametrize("merge,ks", [("0", "1"), ("1", "1"), ("1", "2"), ("1", "4")])
+def test_ctx4096_sixteen_splits_wo_ksplit(gpu, oracle, monkeypatch, merge, ks):
+    """ctx 4096 (16 splits per head), GQA-4 Llama-3-8B shapes (batch 1: run as GQA-2 groups), 2 layers: the
+    default (merge 0: the attention's last arriver merges, wo stages a plain input) and the wo-side merges
+    (the NS = 16 batch), unsplit and K-split."""
+    monkeypatch.setenv("SLI_WO_MERGE", merge)
     monkeypatch.setenv("SLI_WO_KSPLIT", ks)
     om, gm = _models(oracle, "llama3-8b", "f16", "f16", seed=1, num_hidden_layers=2, vocab_size=32000)
     om.fill_kv_synthetic(7, 4095)
