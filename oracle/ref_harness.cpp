@@ -143,6 +143,7 @@ struct RefModel {
     std::shared_ptr<op::argmaxLayer> argmax;
     std::vector<LayerP> norms, wq, wk, wv, wo, up, gate, down;
     std::map<int, mem::Tensor> buf;
+    std::vector<float> kv_store[2];  // the K / V caches' memory (see ref_model_create)
     double t_emb = 0, t_layers = 0, t_head = 0;  // last forward, seconds (harness instrumentation)
     const mem::Tensor& get(Buf t) const { return buf.at(int(t)); }
 };
@@ -279,7 +280,15 @@ static void* create(RefModel* m, int vocab, int dim, int n_heads, int n_kv_heads
     auto alloc = mem::CPUDeviceAllocatorFactory::get_instance();
     auto put = [&](Buf t, std::vector<int32_t> dims) { m->buf.emplace(int(t), mem::Tensor(dims, true, alloc)); };
     put(input_token, {1}); put(position, {1});
-    put(key_cache, {n_layers, max_len, kv}); put(value_cache, {n_layers, max_len, kv});
+    // The K / V caches: model.cpp:264-265 allocates exactly [L][T][KV]. Under GQA rope_kernel.cpp:27 rotates k
+    // over D floats, so a step at position T - 1 of the last layer writes D - KV floats past the end of the cache
+    // (a heap overflow in the reference itself). The harness gives the caches D floats of slack so
+    // timing that step (the CPU baseline at pos ctx - 1) cannot corrupt the heap; every value read is the same.
+    for (int i = 0; i < 2; i++) {
+        m->kv_store[i].assign(size_t(n_layers) * max_len * kv + dim, 0.0f);
+        m->buf.emplace(int(i == 0 ? key_cache : value_cache),
+                       view(m->kv_store[i].data(), {n_layers, max_len, kv}));
+    }
     put(emb_output, {dim}); put(rms_output, {dim}); put(query, {dim});
     // model.cpp:278 sizes the score scratch {head_dim, max_length} but mha uses it as [n_heads][max_length]
     put(score, {std::max(head_dim, n_heads), max_len});
