@@ -43,9 +43,11 @@ FAMILY_KERNELS = {
     False: {"step": "ps_step_kernel (the whole decode step as one persistent launch: 5 phases x 32 layers + LM head)",
             "qkv": "gemv_kernel<EpiQKV> (RMSNorm + [wq;wk;wv] GEMV + RoPE + K/V write)",
             "attention": "attn_partial_kernel (split-context flash decode + last-arriver merge)",
-            "wo": "gemv_kernel<EpiStore, U=2> (wo GEMV + residual add)",
-            "gate_up": "gemv_kernel<EpiSwiGLU> (RMSNorm + [gate;up] GEMV + sigmoid(g)*u)",
-            "down": "gemv_kernel<EpiStore, U=6> (down GEMV + residual add)",
+            "wo": "gemv_merge_kernel<EpiKPart> (attention split merge while staging + K-split wo GEMV -> 2 partial "
+                  "rows; past 8 splits per head: the attention merges and wo is gemv_kernel<EpiStore>)",
+            "gate_up": "gemv_sum_kernel<EpiSwiGLU> (residual + wo partials staged, RMSNorm + [gate;up] GEMV + "
+                       "sigmoid(g)*u)",
+            "down": "gemv_kernel<EpiStoreSum> (down GEMV + residual + wo partials -> x)",
             "lm_head": "gemv_kernel<EpiLogits> (RMSNorm + tied LM head + argmax keys)"},
     True: {"qkv": "bgemm_kernel<BgEpiQKV> (MFMA 16x16x32 f16)", "attention": "attn_partial_kernel (batched kv heads)",
            "wo": "bgemm_kernel<BgEpiStore> (MFMA)", "gate_up": "bgemm_kernel<BgEpiSwiGLU> (MFMA)",
@@ -77,8 +79,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample budget")
     ap.add_argument("--gemv-iters", type=int, default=20)
     ap.add_argument("--traffic-json", default=next(
-        (p for p in (os.path.join(ROOT, "profiles", f) for f in ("r3_gemv_traffic.json", "r2d_gemv_traffic.json"))
-         if os.path.exists(p)), os.path.join(ROOT, "profiles", "r3_gemv_traffic.json")))
+        (p for p in (os.path.join(ROOT, "profiles", f) for f in ("r4_gemv_traffic.json", "r4a_gemv_traffic.json",
+                                                                   "r3_gemv_traffic.json"))
+         if os.path.exists(p)), os.path.join(ROOT, "profiles", "r4a_gemv_traffic.json")))
     return ap.parse_args()
 
 

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Float64 restatement of the C4 decode step for one sequence, as a committed fixture.
 
-    python tests/golden/make_f64_c4.py          # ~5 min, ~12 GB of host memory
+    python tests/golden/make_f64_c4.py          # ~10 min, ~16 GB of host memory
 
 The C4 full-model test bounds the GPU against the oracle. At a context of two positions (sequence 5 of that
 test, position 1) 32 layers of Llama-3-8B amplify the difference between the oracle's sequential fp32 sums and
@@ -9,7 +9,8 @@ the GPU's tree sums to ~1.4e-3 on |logit| ~5.7. Which side carries it? This scri
 Llama-3-8B weights of the synthetic generator (include/sli_synth.h through oracle.synth_fill, fp16-rounded as
 the device holds them; norms fp32), the KV rows 0..pos-1 of sequence 5 (seed 12, fp16), the reference's fp32
 RoPE table — in float64 (model.cpp:40-140 op order; the new K/V row rounded to fp16 as the cache stores it), and
-stores the logits together with the oracle's own error against them. tests/test_gpu_batch.py then bounds the
+stores the logits together with the oracle's own error against them, and the errors of six further fp32
+restatements that differ only in their dot-product summation order (the step's fp32 conditioning). tests/test_gpu_batch.py then bounds the
 GPU's sequence-5 logits against these float64 logits.
 """
 import os
@@ -52,45 +53,91 @@ def main():
     om.close()
     print(f"oracle forward {time.time() - t0:.0f} s", flush=True)
     sin_t, cos_t = O.rope_cache(hd, T, cfg.rope_theta)  # the reference's float32 table (rope_kernel.cpp:4-19)
-    s, c = sin_t[POS].astype(np.float64), cos_t[POS].astype(np.float64)
+    # The float64 step, and beside it SIX legitimate fp32 restatements of the same step that differ only in the
+    # order of their dot-product sums (BLAS sgemv over the whole row, or the row cut into c equal column blocks
+    # summed block by block, c = 2 .. 64): their spread against float64 is the step's own fp32 conditioning, the
+    # scale any fp32 implementation (the oracle's sequential sums, the GPU's tree sums) is judged on.
+    paths = [("f64", np.float64, 0)] + [(f"f32/c{c}", np.float32, c) for c in (1, 2, 4, 8, 16, 64)]
 
-    def rope(v):  # rope_kernel.cpp:22-41
+    def mm(W, h, dt, c):
+        if dt == np.float64:
+            return W @ h
+        if c <= 1:
+            return W @ h
+        K = W.shape[1]
+        acc = np.zeros(W.shape[0], np.float32)
+        for j in range(c):
+            sl = slice(j * K // c, (j + 1) * K // c)
+            acc += W[:, sl] @ h[sl]
+        return acc
+
+    def rms(x, w, dt):
+        return (x / np.sqrt(np.mean(x * x, dtype=dt) + dt(cfg.rms_norm_eps)) * w).astype(dt)
+
+    def rope_dt(v, dt):
+        sv, cv = sin_t[POS].astype(dt), cos_t[POS].astype(dt)
         v = v.reshape(-1, hd).copy()
         a, b = v[:, :hd // 2].copy(), v[:, hd // 2:].copy()
-        v[:, :hd // 2] = a * c - b * s
-        v[:, hd // 2:] = b * c + a * s
+        v[:, :hd // 2] = a * cv - b * sv
+        v[:, hd // 2:] = b * cv + a * sv
         return v.ravel()
 
-    emb = w16(O.T_EMB, 0, V * D, 0.02).reshape(V, D)
-    x = emb[TOKEN].copy()
+    def f16(v, dt):
+        return v.astype(np.float16).astype(dt)
+
     cD, cI = 1.0 / np.sqrt(D), 1.0 / np.sqrt(I)
+    emb = w16(O.T_EMB, 0, V * D, 0.02).reshape(V, D)
+    xs = {n: emb[TOKEN].astype(dt) for n, dt, _ in paths}
     for l in range(L):
-        h = rmsnorm(x, w16(O.T_NORM, 2 * l, D, 0.1, 1.0, f16=False), cfg.rms_norm_eps)
-        q = rope(w16(O.T_WQ, l, D * D, cD).reshape(D, D) @ h)
-        k = rope(w16(O.T_WK, l, KV * D, cD).reshape(KV, D) @ h).astype(np.float16).astype(np.float64)
-        v = (w16(O.T_WV, l, KV * D, cD).reshape(KV, D) @ h).astype(np.float16).astype(np.float64)
-        K = np.concatenate([krows[l], k[None]], 0)  # [pos + 1][KV]
-        Vv = np.concatenate([vrows[l], v[None]], 0)
-        attn = np.empty(D)
-        for hh in range(H):  # mha_kernel.cpp:36-77
-            kv = hh // g
-            sc = K[:, kv * hd:(kv + 1) * hd] @ q[hh * hd:(hh + 1) * hd] / np.sqrt(hd)
-            p = np.exp(sc - sc.max())
-            attn[hh * hd:(hh + 1) * hd] = (p / p.sum()) @ Vv[:, kv * hd:(kv + 1) * hd]
-        x1 = x + w16(O.T_WO, l, D * D, cD).reshape(D, D) @ attn
-        h = rmsnorm(x1, w16(O.T_NORM, 2 * l + 1, D, 0.1, 1.0, f16=False), cfg.rms_norm_eps)
-        u = w16(O.T_UP, l, I * D, cD).reshape(I, D) @ h
-        gt = w16(O.T_GATE, l, I * D, cD).reshape(I, D) @ h
-        x = x1 + w16(O.T_DOWN, l, D * I, cI).reshape(D, I) @ (u / (1.0 + np.exp(-gt)))  # swiglu_kernel.cpp:12-13
+        Wn1 = w16(O.T_NORM, 2 * l, D, 0.1, 1.0, f16=False)
+        Wn2 = w16(O.T_NORM, 2 * l + 1, D, 0.1, 1.0, f16=False)
+        Wq = w16(O.T_WQ, l, D * D, cD).reshape(D, D)
+        Wk = w16(O.T_WK, l, KV * D, cD).reshape(KV, D)
+        Wv = w16(O.T_WV, l, KV * D, cD).reshape(KV, D)
+        Wo = w16(O.T_WO, l, D * D, cD).reshape(D, D)
+        Wu = w16(O.T_UP, l, I * D, cD).reshape(I, D)
+        Wg = w16(O.T_GATE, l, I * D, cD).reshape(I, D)
+        Wd = w16(O.T_DOWN, l, D * I, cI).reshape(D, I)
+        W32 = {k: v.astype(np.float32) for k, v in dict(q=Wq, k=Wk, v=Wv, o=Wo, u=Wu, g=Wg, d=Wd).items()}
+        W64 = dict(q=Wq, k=Wk, v=Wv, o=Wo, u=Wu, g=Wg, d=Wd)
+        for n, dt, c in paths:
+            Wm = W64 if dt == np.float64 else W32
+            x = xs[n]
+            h = rms(x, Wn1.astype(dt), dt)
+            q = rope_dt(mm(Wm["q"], h, dt, c), dt)
+            k = f16(rope_dt(mm(Wm["k"], h, dt, c), dt), dt)
+            v = f16(mm(Wm["v"], h, dt, c), dt)
+            K = np.concatenate([krows[l].astype(dt), k[None]], 0)  # [pos + 1][KV]
+            Vv = np.concatenate([vrows[l].astype(dt), v[None]], 0)
+            attn = np.empty(D, dt)
+            for hh in range(H):  # mha_kernel.cpp:36-77
+                kv = hh // g
+                sc = (K[:, kv * hd:(kv + 1) * hd] @ q[hh * hd:(hh + 1) * hd] / dt(np.sqrt(hd))).astype(dt)
+                p = np.exp(sc - sc.max())
+                attn[hh * hd:(hh + 1) * hd] = (p / p.sum()) @ Vv[:, kv * hd:(kv + 1) * hd]
+            x1 = x + mm(Wm["o"], attn, dt, c)
+            h = rms(x1, Wn2.astype(dt), dt)
+            u = mm(Wm["u"], h, dt, c)
+            gt = mm(Wm["g"], h, dt, c)
+            xs[n] = x1 + mm(Wm["d"], (u / (dt(1.0) + np.exp(-gt))).astype(dt), dt, c)  # swiglu_kernel.cpp:12-13
         print(f"layer {l} {time.time() - t0:.0f} s", flush=True)
-    logits = emb @ rmsnorm(x, w16(O.T_NORM, 2 * L, D, 0.1, 1.0, f16=False), cfg.rms_norm_eps)
+    wl = w16(O.T_NORM, 2 * L, D, 0.1, 1.0, f16=False)
+    logits = emb @ rmsnorm(xs["f64"], wl, cfg.rms_norm_eps)
+    emb32 = emb.astype(np.float32)
+    spread = []
+    for n, dt, c in paths[1:]:
+        lg = mm(emb32, rms(xs[n], wl.astype(np.float32), np.float32), np.float32, c)
+        spread.append(float(np.abs(lg - logits).max()))
+        print(f"{n}: vs float64 max|d| {spread[-1]:.3e}")
     err = float(np.abs(want32 - logits).max())
     print(f"oracle (fp32 sequential) vs float64: max|d| {err:.3e}, |logit|max {np.abs(logits).max():.3f}, "
           f"argmax {int(np.argmax(want32))} vs {int(np.argmax(logits))}")
     # float32 copy of the float64 logits (6e-8 relative: far inside the 1e-3 bar it serves)
     np.savez_compressed(os.path.join(HERE, "c4_f64_seq5.npz"), logits=logits.astype(np.float32),
                         token=np.int32(TOKEN), pos=np.int32(POS), kv_seed=np.int32(KV_SEED), seed=np.int32(SEED),
-                        oracle_err=np.float64(err), argmax=np.int32(np.argmax(logits)))
+                        oracle_err=np.float64(err), argmax=np.int32(np.argmax(logits)),
+                        fp32_spread=np.array(spread, np.float64),
+                        fp32_paths=np.array([n for n, _, _ in paths[1:]]))
 
 
 if __name__ == "__main__":

@@ -156,12 +156,13 @@ def test_llama3_8b_full_batch8_matches_oracle(gpu, oracle):
     oracle's full forward per sequence (the lazy oracle: each layer's weights regenerated in turn), ragged
     positions. Bar: the same argmax for every sequence and logits within 1e-3 absolute (north star: "1e-3 fp16
     tolerance"). Sequence 5 sits at position 1. A float64 restatement of that step (tests/golden/make_f64_c4.py,
-    committed as c4_f64_seq5.npz) puts the ORACLE 1.33e-3 from float64 and the GPU 1.36e-3 (round 4): both fp32
-    paths sit the same distance from float64, so the 1.4e-3 is the step's own conditioning at a two-position
+    committed as c4_f64_seq5.npz) puts the ORACLE 1.33e-3 from float64, six further fp32 restatements that differ
+    only in their dot-product summation order 1.04e-3 .. 1.34e-3 (fp32_spread), and the GPU 1.36e-3 (round 4):
+    every fp32 path sits that far from float64, so the 1.4e-3 is the step's own conditioning at a two-position
     context (each layer's new K/V row, half of the attention's input, is rounded to fp16 from an fp32 value;
     32 layers amplify which side of a rounding boundary it lands on), not an error of either side. That
-    sequence is therefore bounded by the oracle's own float64 distance: GPU vs float64 within 1.1x of it, and
-    GPU vs oracle within 1e-3 plus it."""
+    sequence is therefore bounded by the fp32 paths' own float64 distance: GPU vs float64 within 1.1x of the
+    largest of them, and GPU vs oracle within 1e-3 plus the oracle's."""
     import os
     from simplellminference_amd.model import LlamaModel, preset
     f64 = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c4_f64_seq5.npz"))
@@ -175,7 +176,8 @@ def test_llama3_8b_full_batch8_matches_oracle(gpu, oracle):
     gm.close()
     err64 = float(np.abs(got[5] - f64["logits"]).max())
     print(f"C4 sequence 5 (pos 1): GPU vs float64 max|d| {err64:.2e}; oracle vs float64 {float(f64['oracle_err']):.2e}")
-    assert err64 <= 1.1 * float(f64["oracle_err"]), err64
+    fp32_worst = max(float(f64["oracle_err"]), float(np.max(f64["fp32_spread"])))
+    assert err64 <= 1.1 * fp32_worst, (err64, fp32_worst)
     assert int(np.argmax(got[5])) == int(f64["argmax"])
     om = oracle.Model(_ocfg(oracle, cfg), seed=1, wmode=oracle.W_F16, kv_f16=True, lazy=True)
     errs = []
