@@ -66,6 +66,10 @@ struct BgIn {
     float* ws;            // splits > 1: partials [ntiles][splits][16][8]
     unsigned* counters;   // splits > 1: [groups] arrival counters, zero between launches
     unsigned long long* stamps = nullptr;  // diagnostic (tools/bgemm_lab): per-workgroup s_memrealtime x4
+    // W in the fragment layout (bg_tile_kernel): tile t's k-block kb is 1 KiB at ((t * K/32) + kb) * 1024, lane l's
+    // 16-byte A operand at l * 16 — one wave load is one contiguous KiB (8 full 128-B lines) instead of 16 rows x
+    // 64 B (16 half lines). 0: W row-major [rows][K] (the op-level entry, tools/bgemm_lab)
+    int tiled = 0;
 };
 
 // ---------------------------------------------------------------- host-side plan
@@ -226,15 +230,21 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
     // ---- 2. the first two weight steps
     const size_t row_bytes = (size_t)K * 2;
     const int q8 = (lane >> 4) * 8;  // this lane's k offset inside a 32-k block
+    const size_t bstride = in.tiled ? 1024 : 64;  // bytes between a lane's consecutive k-blocks
     auto load_step = [&](int k, u32x4(&w)[kBgU]) {
         const int kk = min(k, nsteps - 1);
         const int j = kk / cpt, c = kk - j * cpt;
-        const int row = epi.row(t0 + j, lane & 15);
-        const char* base = reinterpret_cast<const char*>(W) + (size_t)row * row_bytes + (size_t)q8 * 2;
+        const char* base;
+        if (in.tiled) {
+            base = reinterpret_cast<const char*>(W) + (size_t)(t0 + j) * nkb * 1024 + (size_t)lane * 16;
+        } else {
+            const int row = epi.row(t0 + j, lane & 15);
+            base = reinterpret_cast<const char*>(W) + (size_t)row * row_bytes + (size_t)q8 * 2;
+        }
 #pragma unroll
         for (int u = 0; u < kBgU; ++u) {
             const int bi = wb0 + min(c * kBgU + u, max(wnb - 1, 0));
-            w[u] = load16<true>(base + (size_t)bi * 64);
+            w[u] = load16<true>(base + (size_t)bi * bstride);
         }
     };
     u32x4 wa[kBgU], wb[kBgU];  // (a third step in flight measured slower: C4 1660 -> 1546 tok/s)
@@ -498,6 +508,35 @@ struct BgEpiLogits {
         if ((int)threadIdx.x < B) keys_out[(size_t)threadIdx.x * key_ld + g] = kl[threadIdx.x];
     }
 };
+
+// Row-major W [rows][K] -> the fragment layout of BgIn::tiled, rows in the epilogue's tile order (Epi::row:
+// RoPE pairs, gate/up pairs, the last tile's clamped rows): out[(t * K/32 + kb) * 64 + l] (16-byte pieces) =
+// W[row(t, l & 15)][32 kb + 8 (l >> 4) .. + 7]. Init-time only (weights placed or replaced).
+template <class Epi>
+__global__ void __launch_bounds__(256) bg_tile_kernel(const __half* __restrict__ W, int K, int ntiles, Epi epi,
+                                                       uint4* __restrict__ out) {
+    const int nkb = K / 32;
+    const size_t n = (size_t)ntiles * nkb * 64;
+    for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
+        const int l = (int)(p & 63);
+        const size_t tb = p >> 6;
+        const int t = (int)(tb / nkb), kb = (int)(tb - (size_t)t * nkb);
+        const int row = epi.row(t, l & 15);
+        out[p] = *reinterpret_cast<const uint4*>(W + (size_t)row * K + (size_t)kb * 32 + 8 * (l >> 4));
+    }
+}
+
+template <class Epi>
+hipError_t launch_bg_tile(const __half* W, int K, int ntiles, const Epi& epi, void* out, hipStream_t s) {
+    if (K % 32) return hipErrorInvalidValue;
+    const size_t n = (size_t)ntiles * (K / 32) * 64;
+    const int blocks = (int)std::min<size_t>(8192, (n + 255) / 256);
+    hipLaunchKernelGGL((bg_tile_kernel<Epi>), dim3(blocks), dim3(256), 0, s, W, K, ntiles, epi,
+                       reinterpret_cast<uint4*>(out));
+    return hipGetLastError();
+}
+// bytes of a tiled matrix
+inline size_t bg_tiled_bytes(int ntiles, int K) { return (size_t)ntiles * (size_t)(K / 32) * 1024; }
 
 // Allow the kernel its full dynamic LDS (once per instantiation; call outside stream capture).
 template <class Epi, bool NORM>

@@ -46,6 +46,9 @@ struct LayerW {
     float* gu_s = nullptr;
     void* down = nullptr;  // [D][Il]      (column slice of down)
     float* down_s = nullptr;
+    // batch > 1, fp16: the same matrices in bgemm's fragment layout (bgemm.h BgIn::tiled), rows in each
+    // epilogue's tile order; the decode step streams these, the row-major copies serve prefill-free readback
+    void *qkv_t = nullptr, *wo_t = nullptr, *gu_t = nullptr, *down_t = nullptr;
 };
 
 }  // namespace sli
@@ -65,6 +68,9 @@ struct sli_model {
     // device buffers
     void* emb = nullptr;
     float* emb_s = nullptr;
+    void* lm_t = nullptr;     // batch > 1: this rank's LM-head rows of emb in the fragment layout (LayerW::*_t)
+    bool bg_tiled = false;    // the batched projections stream the fragment-layout copies
+    bool tiles_dirty = false; // a weight was placed since the copies were last built (bg_sync_tiles)
     float* norms = nullptr;
     std::vector<sli::LayerW> layers;
     void* kc = nullptr;
@@ -333,6 +339,7 @@ static int place_tensor(sli_model* m, int kind, int index, const Src& src) {
     }
     sli_shard_window w;
     SLI_TRY(sli_tp_plan(&m->c, kind, &w));
+    m->tiles_dirty = m->bg_tiled;
     if (kind == SLI_T_EMB)
         return place(m, m->emb, m->emb_s, w.n_rows, w.n_cols, w.row_lo, w.col_lo, w.full_cols, src);
     if (index < 0 || index >= m->L) return fail(SLI_ERR_RANGE, "layer index");
@@ -726,31 +733,32 @@ struct StepRecorder {
         in.B = m->B;
         in.ws = m->bg_ws;
         in.counters = m->bg_cnt;
+        in.tiled = m->bg_tiled ? 1 : 0;
         return in;
     }
     static int b_qkv(sli_model* m, int l) {
         const size_t lay = (size_t)l * m->B * m->hkv * m->T * m->hd;
         BgEpiQKV<KT> e{m->q, (KT*)m->kc + lay, (KT*)m->vc + lay, &m->st->pos, kPosStride, m->sin_t, m->cos_t,
                        m->hq, m->hkv, m->hd, m->T};
-        return bg(m, m->layers[l].qkv, bin(m, m->x, m->norms + (size_t)(2 * l) * m->D, m->D), e, m->bp_qkv);
+        return bg(m, m->bg_tiled ? m->layers[l].qkv_t : m->layers[l].qkv, bin(m, m->x, m->norms + (size_t)(2 * l) * m->D, m->D), e, m->bp_qkv);
     }
     static int b_wo(sli_model* m, int l) {
         const bool tp = m->partial;
         BgEpiStore e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, nullptr, 1.0f, m->D, m->D};
-        return bg(m, m->layers[l].wo, bin(m, m->attn, nullptr, m->hq * m->hd), e, m->bp_wo);
+        return bg(m, m->bg_tiled ? m->layers[l].wo_t : m->layers[l].wo, bin(m, m->attn, nullptr, m->hq * m->hd), e, m->bp_wo);
     }
     static int b_gu(sli_model* m, int l) {
         BgEpiSwiGLU e{m->act, m->Il, m->c.act_mode};
-        return bg(m, m->layers[l].gu, bin(m, m->x, m->norms + (size_t)(2 * l + 1) * m->D, m->D), e, m->bp_gu);
+        return bg(m, m->bg_tiled ? m->layers[l].gu_t : m->layers[l].gu, bin(m, m->x, m->norms + (size_t)(2 * l + 1) * m->D, m->D), e, m->bp_gu);
     }
     static int b_down(sli_model* m, int l) {
         const bool tp = m->partial;
         BgEpiStore e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, nullptr, 1.0f, m->D, m->D};
-        return bg(m, m->layers[l].down, bin(m, m->act, nullptr, m->Il), e, m->bp_down);
+        return bg(m, m->bg_tiled ? m->layers[l].down_t : m->layers[l].down, bin(m, m->act, nullptr, m->Il), e, m->bp_down);
     }
     static int b_lm(sli_model* m) {
         BgEpiLogits e{m->logits, m->keys, m->v_n, m->v_n, m->v_lo, m->key_ld};
-        const void* w = wptr(m->emb, m->wbytes, (size_t)m->v_lo * m->D);
+        const void* w = m->bg_tiled ? m->lm_t : wptr(m->emb, m->wbytes, (size_t)m->v_lo * m->D);
         return bg(m, w, bin(m, m->x, m->norms + (size_t)(2 * m->L) * m->D, m->D), e, m->bp_lm);
     }
     // ---- one step = phases 0 .. 2L (model.cpp:48-139). Phase 2l: [embedding when l = 0,] qkv(l),
@@ -1093,12 +1101,44 @@ static int capture_graph(hipStream_t stream, hipGraph_t& graph, hipGraphExec_t& 
     return SLI_OK;
 }
 
+// (Re)build the fragment-layout copies of the batched projections from the row-major matrices after weights
+// were placed (bgemm.h bg_tile_kernel; each epilogue's row order), on the model's stream before any use
+static int bg_sync_tiles(sli_model* m) {
+    if (!m->bg_tiled || !m->tiles_dirty) return SLI_OK;
+    const int D = m->D, hd = m->hd, QD = m->hq * hd;
+    hipStream_t s = m->stream;
+    BgEpiQKV<__half> eq{};
+    eq.hq = m->hq;
+    eq.hkv = m->hkv;
+    eq.hd = hd;
+    BgEpiStore eo{};
+    eo.nrows = D;
+    BgEpiSwiGLU eg{};
+    eg.inter = m->Il;
+    BgEpiLogits el{};
+    el.nrows = m->v_n;
+    for (const LayerW& w : m->layers) {
+        SLI_HIP(launch_bg_tile((const __half*)w.qkv, D, m->bp_qkv.ntiles, eq, w.qkv_t, s));
+        SLI_HIP(launch_bg_tile((const __half*)w.wo, QD, m->bp_wo.ntiles, eo, w.wo_t, s));
+        SLI_HIP(launch_bg_tile((const __half*)w.gu, D, m->bp_gu.ntiles, eg, w.gu_t, s));
+        SLI_HIP(launch_bg_tile((const __half*)w.down, m->Il, m->bp_down.ntiles, eo, w.down_t, s));
+    }
+    SLI_HIP(launch_bg_tile((const __half*)m->emb + (size_t)m->v_lo * D, D, m->bp_lm.ntiles, el, m->lm_t, s));
+    m->tiles_dirty = false;
+    return SLI_OK;
+}
+
 static int capture(sli_model* m) {
+    SLI_TRY(bg_sync_tiles(m));
     return capture_graph(m->stream, m->graph, m->graph_exec, [&]() { return SLI_DISPATCH(m, record, m); });
 }
 
 static int capture_group(sli_tp_group* g) {
     sli_model* m0 = g->ranks[0];
+    for (sli_model* r : g->ranks) {
+        SLI_TRY(bg_sync_tiles(r));
+        SLI_HIP(hipStreamSynchronize(r->stream));
+    }
     return capture_graph(g->stream, g->graph, g->exec, [&]() { return SLI_DISPATCH(m0, record_group, g); });
 }
 
@@ -1312,6 +1352,18 @@ static int create_model(const sli_model_config* cfg, const void* comm_id, sli_tp
         }
         m->key_ld = std::max(m->key_ld, m->bp_lm.groups);
         A((void**)&m->bg_ws, bg_part + 256);
+        // the fragment-layout copies (SLI_BG_TILED=0: stream the row-major matrices, 16 rows x 64 B per wave load)
+        const char* te = getenv("SLI_BG_TILED");
+        m->bg_tiled = !(te && te[0] == '0') && c.w_dtype == SLI_DT_F16;
+        if (m->bg_tiled) {
+            for (auto& w : m->layers) {
+                A(&w.qkv_t, bg_tiled_bytes(m->bp_qkv.ntiles, D));
+                A(&w.wo_t, bg_tiled_bytes(m->bp_wo.ntiles, m->hq * hd));
+                A(&w.gu_t, bg_tiled_bytes(m->bp_gu.ntiles, D));
+                A(&w.down_t, bg_tiled_bytes(m->bp_down.ntiles, m->Il));
+            }
+            A(&m->lm_t, bg_tiled_bytes(m->bp_lm.ntiles, D));
+        }
         A((void**)&m->bg_cnt, sizeof(unsigned) * bg_groups);
     }
     A((void**)&m->bkeys, sizeof(unsigned long long) * B);
@@ -1990,6 +2042,7 @@ int sli_model_time_families(sli_model* m, int32_t iters, double* us, double* byt
     SLI_CHECK(m && iters > 0 && us && bytes && launches, SLI_ERR_ARG, "bad argument");
     SLI_CHECK(!m->group, SLI_ERR_STATE, "time a group's ranks through a standalone model");
     SLI_HIP(hipSetDevice(m->c.device));
+    SLI_TRY(bg_sync_tiles(m));
     // Like sli_model_time_gemv: x is saved and restored; the qkv family rewrites each layer's K/V row at
     // the current position, which the next real step at that position rewrites again.
     struct Guard {
