@@ -476,13 +476,23 @@ struct GroupSumArgs {
     const float* src[kMaxGroup];  // rank r's partial [B*D] (rank 0's includes the residual)
     float* dst[kMaxGroup];        // rank r's residual stream x
     int n_ranks, n;
+    int f16_payload = 0;  // debug (SLI_DEBUG_AR_F16): each rank's contribution rounded to fp16 as an
+                          // fp16 exchange would carry it (the residual stays fp32, added once locally)
 };
 
 // x_r = ((p_0 + p_1) + p_2) + ... for every rank r: one fixed order, so every rank holds the same x
 __global__ void __launch_bounds__(256) group_sum_kernel(GroupSumArgs a) {
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
-        float s = a.src[0][i];
-        for (int r = 1; r < a.n_ranks; ++r) s += a.src[r][i];
+        float s;
+        if (a.f16_payload) {  // x + sum_r fp16(p_r), p_0 = rank 0's partial without the residual it added
+            const float x = a.dst[0][i];
+            s = __half2float(__float2half(a.src[0][i] - x));
+            for (int r = 1; r < a.n_ranks; ++r) s += __half2float(__float2half(a.src[r][i]));
+            s = x + s;
+        } else {
+            s = a.src[0][i];
+            for (int r = 1; r < a.n_ranks; ++r) s += a.src[r][i];
+        }
         for (int r = 0; r < a.n_ranks; ++r) a.dst[r][i] = s;
     }
 }
@@ -862,6 +872,7 @@ struct StepRecorder {
         GroupSumArgs sa{};
         sa.n_ranks = n;
         sa.n = m0->B * m0->D;
+        sa.f16_payload = getenv("SLI_DEBUG_AR_F16") ? 1 : 0;
         GroupKeyArgs ka{};
         ka.n_ranks = n;
         ka.B = m0->B;

@@ -3,7 +3,7 @@
 // distinct weight copies inside a replayed hipGraph (no Infinity-Cache re-reads). Prints us per launch
 // and GB/s of algorithmic weight bytes.
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include tools/bgemm_lab.hip -o tools/bgemm_lab
-//   tools/bgemm_lab [batch]
+//   tools/bgemm_lab [batch]          (LAB_TILED=1: the weights in the fragment layout, BgIn::tiled)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -48,6 +48,7 @@ static double time_cfg(const std::vector<__half*>& Ws, int rows, int K, int B, b
     hipStream_t s;
     CK(hipStreamCreate(&s));
     BgIn in{x, norm ? nw : nullptr, 1e-5f, K, B, 0, 0, 0, ws, cnt};
+    in.tiled = getenv("LAB_TILED") ? 1 : 0;
     BgEpiStore e{y, nullptr, nullptr, 1.0f, rows, rows};
     CK((bg_allow_lds<BgEpiStore, true>()));
     CK((bg_allow_lds<BgEpiStore, false>()));
@@ -94,7 +95,7 @@ int main(int argc, char** argv) {
     fill_f<<<256, 256>>>(nw, 16384, 5, 1.0f);
     for (const Shape& sh : shapes) {
         std::vector<__half*> Ws(NL);
-        const size_t n = (size_t)sh.rows * sh.K;
+        const size_t n = (size_t)((sh.rows + 15) / 16) * 16 * sh.K;  // whole tiles (the fragment layout's size)
         for (int l = 0; l < NL; ++l) {
             CK(hipMalloc(&Ws[l], n * 2));
             fill_h<<<1024, 256>>>(Ws[l], n, 11 + l);
@@ -139,6 +140,7 @@ int main(int argc, char** argv) {
             CK(hipMalloc(&st, sizeof(unsigned long long) * 4 * nwg));
             CK(hipMemset(st, 0, sizeof(unsigned long long) * 4 * nwg));
             BgIn in{x, sh.norm ? nw : nullptr, 1e-5f, sh.K, B, 0, 0, 0, ws, cnt, st};
+            in.tiled = getenv("LAB_TILED") ? 1 : 0;
             BgEpiStore e{y, nullptr, nullptr, 1.0f, sh.rows, sh.rows};
             CK(launch_bgemm(Ws[0], in, e, p, 0));
             CK(hipDeviceSynchronize());
