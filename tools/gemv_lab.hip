@@ -410,6 +410,68 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
+    if (mode == "tp8") {
+        // the TP-8 shard GEMVs as the engine launches them (launch_gemv_u: the column split at these sizes), per
+        // launch phase stamps, beside the streaming-read floor of the same bytes: where a small launch's time goes
+        const int nst = 256 * 16 * 4;
+        unsigned long long* st;
+        CK(hipMalloc(&st, (size_t)NL * nst * 8));
+        std::vector<unsigned long long> h((size_t)NL * nst);
+        struct T8 { const char* name; int si, rows, cols, R; bool norm; };
+        const T8 t8[] = {{"tp8-qkv", 0, 1536, 4096, 2, true}, {"tp8-wo", 1, 4096, 512, 1, false},
+                         {"tp8-gu", 2, 2752, 4096, 2, true}, {"tp8-down", 3, 4096, 1376, 1, false},
+                         {"tp4-qkv", 0, 3072, 4096, 2, true}, {"tp4-gu", 2, 5504, 4096, 2, true},
+                         {"tp2-gu", 2, 11008, 4096, 2, true}, {"tp1-qkv", 0, 12288, 4096, 2, true},
+                         {"tp1-down", 3, 4096, 11008, 1, false}};
+        for (const T8& t : t8) {
+            const long long bytes = (long long)t.rows * t.cols * 2;
+            auto launch = [&](int l, unsigned long long* stp) {
+                GemvIn in{x, t.norm ? nw : nullptr, 1e-5f, t.cols};
+                in.stamps = stp;
+                if (t.R == 2) {
+                    EpiStore<2> e{y, nullptr, nullptr, 1.0f, t.rows};
+                    CK((launch_gemv_u<__half, 2, 4, true>(w[t.si][l], in, e, t.rows / 2, s)));
+                } else if (t.si == 1) {
+                    EpiStore<1> e{y, nullptr, nullptr, 1.0f, t.rows};
+                    CK((launch_gemv_u<__half, 1, 2, true>(w[t.si][l], in, e, t.rows, s)));
+                } else {
+                    EpiStore<1> e{y, nullptr, nullptr, 1.0f, t.rows};
+                    CK((launch_gemv_u<__half, 1, 6, true>(w[t.si][l], in, e, t.rows, s)));
+                }
+            };
+            const float g_ms = time_graph(s, [&] { for (int l = 0; l < NL; ++l) launch(l, nullptr); });
+            const float s_ms = time_graph(s, [&] {
+                for (int l = 0; l < NL; ++l)
+                    hipLaunchKernelGGL(stream_kernel<8>, dim3(256), dim3(1024), 0, s, (const char*)w[t.si][l], bytes, y2,
+                                       nullptr);
+            });
+            CK(hipMemset(st, 0, (size_t)NL * nst * 8));
+            time_graph(s, [&] { for (int l = 0; l < NL; ++l) launch(l, st + (size_t)l * nst); }, 1);
+            CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+            std::vector<double> ent, stg, ex;
+            for (int l = 2; l < NL; ++l) {
+                const unsigned long long* q = h.data() + (size_t)l * nst;
+                unsigned long long t0 = ~0ull;
+                for (int i = 0; i < 4096; ++i)
+                    if (q[i * 4 + 3]) t0 = std::min(t0, q[i * 4]);
+                for (int i = 0; i < 4096; ++i) {
+                    if (q[i * 4 + 3] == 0) continue;
+                    ent.push_back((q[i * 4] - t0) * 0.01);
+                    stg.push_back((q[i * 4 + 1] - t0) * 0.01);
+                    ex.push_back((q[i * 4 + 2] - t0) * 0.01);
+                }
+            }
+            std::sort(ent.begin(), ent.end());
+            std::sort(stg.begin(), stg.end());
+            std::sort(ex.begin(), ex.end());
+            auto pc = [](std::vector<double>& v, double f) { return v.empty() ? 0.0 : v[(size_t)(f * (v.size() - 1))]; };
+            printf("%-9s %5.2f MB  gemv %6.2f us  stream %6.2f us | waves %zu: entry p50 %5.2f max %5.2f | staged p50 %5.2f "
+                   "p99 %5.2f | exit p10 %5.2f p50 %5.2f p90 %5.2f max %5.2f\n",
+                   t.name, bytes / 1e6, 1000.0 * g_ms / NL, 1000.0 * s_ms / NL, ent.size() / (NL - 2), pc(ent, .5),
+                   pc(ent, 1.0), pc(stg, .5), pc(stg, .99), pc(ex, .1), pc(ex, .5), pc(ex, .9), pc(ex, 1.0));
+        }
+        return 0;
+    }
     std::vector<Cfg> cfgs = {
         {"R2U4", run_cfg<2, 4, true>}, {"R2U4NB3", run_cfg_nb<2, 4, 3>}, {"R2U2NB4", run_cfg_nb<2, 2, 4>},
         {"R1U6", run_cfg<1, 6, true>}, {"R1U6NB3", run_cfg_nb<1, 6, 3>}, {"R1U4NB3", run_cfg_nb<1, 4, 3>},
