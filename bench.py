@@ -67,10 +67,11 @@ def parse():
     ap.add_argument("--exec", default="launches", choices=["launches", "persistent"],
                     help="launches: one graph of fused launches (default, fastest measured); persistent: the whole "
                          "step as one launch with grid barriers (batch 1, TP 1; DESIGN.md §4)")
-    ap.add_argument("--tp-allreduce", default="auto", choices=["auto", "rccl", "oneshot", "fused"],
-                    help="TP all-reduce: auto = the one-shot exchange fused into the wo / down launches (batch 1; "
-                         "the separate one-shot kernel at batch > 1) if a validation step against RCCL agrees on "
-                         "every rank, else RCCL")
+    ap.add_argument("--tp-allreduce", default="auto", choices=["auto", "rccl", "oneshot", "fused", "fused_wg"],
+                    help="TP all-reduce: auto = the one-shot exchange fused into the wo / down launches (batch 1: "
+                         "per workgroup when every rank has its own GPU, else one summing workgroup; the separate "
+                         "one-shot kernel at batch > 1) if a validation step against RCCL agrees on every rank, "
+                         "else RCCL")
     ap.add_argument("--prefill-tokens", type=int, default=512,
                     help="after the decode timing: prefill a prompt of this many tokens (0: skip; batch 1 only)")
     ap.add_argument("--prefill-reps", type=int, default=3, help="timed prefill repetitions (after one warm-up)")
@@ -181,7 +182,7 @@ def _oneshot_opened(model, dist, torch, mode) -> bool:
         progress(f"one-shot buffers unavailable on this rank: {e}")
     flag = torch.tensor([0 if err else 1], dtype=torch.int32)
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-    if flag.item() == 0 and mode in ("oneshot", "fused"):  # forced one-shot: EVERY rank stops (none waits on RCCL alone)
+    if flag.item() == 0 and mode in ("oneshot", "fused", "fused_wg"):  # forced one-shot: EVERY rank stops (none waits on RCCL alone)
         raise SystemExit(f"one-shot buffers could not be mapped on every rank ({err or 'another rank failed'})")
     return flag.item() == 1
 
@@ -236,7 +237,11 @@ def main():
     allreduce = "none"
     if dist_on:
         allreduce = "rccl"
-        os_mode = a.tp_allreduce if a.tp_allreduce in ("oneshot", "fused") else ("fused" if B == 1 else "oneshot")
+        # auto: batch 1 exchanges inside wo / down, per workgroup when every rank has a GPU of its own (ranks
+        # sharing one would starve each other of CUs), else through one summing workgroup per launch
+        own_gpu = world <= max(1, torch.cuda.device_count())
+        os_mode = (a.tp_allreduce if a.tp_allreduce in ("oneshot", "fused", "fused_wg")
+                   else ("fused_wg" if own_gpu else "fused") if B == 1 else "oneshot")
         if os.environ.get("SLI_DEBUG_NOCOMM") and a.tp_allreduce != "rccl":
             # debug (several ranks on one GPU, no RCCL communicator): the one-shot kernels are the only exchange
             from simplellminference_amd import tp
@@ -257,7 +262,7 @@ def main():
             dist.all_reduce(flag, op=dist.ReduceOp.MIN)
             if flag.item() == 1:
                 allreduce = f"{os_mode} (validated against rccl on every rank)"
-            elif a.tp_allreduce in ("oneshot", "fused"):
+            elif a.tp_allreduce in ("oneshot", "fused", "fused_wg"):
                 raise SystemExit("one-shot all-reduce disagrees with RCCL")
             else:
                 model.set_allreduce("rccl")

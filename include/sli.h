@@ -154,8 +154,12 @@ int sli_tp_vocab(const sli_model_config* cfg, int32_t* vocab_lo, int32_t* vocab_
  * sums in rank order, so every rank holds bit-identical x; the argmax keys use the same exchange.
  * SLI_ALLREDUCE_FUSED (batch 1): the same exchange inside the wo / down GEMV launches — their epilogues
  * push the finished rows into the peers' slots and the launch's last workgroup waits and sums (no
- * separate all-reduce launch). */
-enum { SLI_ALLREDUCE_RCCL = 0, SLI_ALLREDUCE_ONESHOT = 1, SLI_ALLREDUCE_FUSED = 2 };
+ * separate all-reduce launch).
+ * SLI_ALLREDUCE_FUSED_WG (batch 1, ranks on distinct devices): the fused exchange per workgroup — workgroup w
+ * of every rank owns the same rows, waits for the same workgroup of the peers and sums its own rows (no
+ * launch-wide arrival, no single summing workgroup). Every workgroup waits, so ranks sharing one device
+ * would starve each other of CUs unless their grids fit together (SLI_DEBUG_GEMV_MAX_BLOCKS). */
+enum { SLI_ALLREDUCE_RCCL = 0, SLI_ALLREDUCE_ONESHOT = 1, SLI_ALLREDUCE_FUSED = 2, SLI_ALLREDUCE_FUSED_WG = 3 };
 int sli_model_comm_handle_bytes(void);
 int sli_model_comm_handle(sli_model* m, void* out, int32_t n);
 int sli_model_comm_open(sli_model* m, const void* handles, int32_t nranks);

@@ -114,6 +114,7 @@ struct sli_model {
     bool os_open = false;
     bool os_dead = false;                    // a one-shot wait timed out: set_allreduce(ONESHOT) is refused
     unsigned* os_epoch = nullptr;            // one-shot call counter; os_epoch[1..9]: fused-launch arrivals
+    unsigned* os_wg_epoch = nullptr;         // SLI_ALLREDUCE_FUSED_WG: per-(region, workgroup) epochs [2][kOsMaxWg]
     int os_nmax = 0;
     bool os_loopback = false;                // debug: SLI_DEBUG_OS_LOOPBACK (oneshot.h OneShotArgs::loopback)
     char** os_peer_tab = nullptr;            // device copy of os_peer (oneshot.h EpiPush::peer_tab)
@@ -553,7 +554,7 @@ struct StepRecorder {
         if (!m->wo_merge) {  // the attention merged its splits into attn: a plain input
             GemvIn in{m->attn, nullptr, 0.0f, m->hq * m->hd};
             if (fused_ar(m)) {
-                SLI_HIP((launch_gemv_u<WT, 1, 2, NT>((const WT*)w.wo, in, push_epi(m, w.wo_s), m->D, m->stream)));
+                SLI_HIP((launch_gemv_u<WT, 1, 2, NT>((const WT*)w.wo, in, push_epi(m, w.wo_s, 0), m->D, m->stream)));
                 return SLI_OK;
             }
             EpiStore<1> e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, w.wo_s, 1.0f, m->D};
@@ -565,7 +566,7 @@ struct StepRecorder {
         const AttnMergeIn am{m->part, &m->st->pos, attn_max_splits(m), attn_wg_positions(m->c.kv_dtype, m->hd), m->hd};
         constexpr int UW = 2;  // int8 too (tools/gemv_lab i8: R1U2 7.5 us vs R1U1 7.95 on the 4096x4096 shape)
         if (fused_ar(m)) {
-            const EpiPush<1> ep = push_epi(m, w.wo_s);
+            const EpiPush<1> ep = push_epi(m, w.wo_s, 0);
             if (am.max_splits > 8)
                 SLI_HIP((launch_gemv_merge<WT, 1, UW, NT, EpiPush<1>, 16>((const WT*)w.wo, in, ep, am, m->D, m->stream)));
             else
@@ -625,7 +626,7 @@ struct StepRecorder {
         const bool tp = m->partial;
         GemvIn in{m->act, nullptr, 0.0f, m->Il};
         if (fused_ar(m)) {
-            const EpiPush<1> ep = push_epi(m, w.down_s);
+            const EpiPush<1> ep = push_epi(m, w.down_s, 1);
             if constexpr (std::is_same<WT, int8_t>::value)
                 SLI_HIP((launch_gemv<WT, 1, 4, NT>((const WT*)w.down, in, ep, m->D, m->stream)));
             else
@@ -665,8 +666,11 @@ struct StepRecorder {
         return SLI_OK;
     }
     // the residual all-reduce inside the wo / down launch (oneshot.h EpiPush), batch 1
-    static bool fused_ar(const sli_model* m) { return m->partial && m->ar_mode == SLI_ALLREDUCE_FUSED; }
-    static EpiPush<1> push_epi(sli_model* m, const float* rscale) {
+    static bool fused_ar(const sli_model* m) {
+        return m->partial && (m->ar_mode == SLI_ALLREDUCE_FUSED || m->ar_mode == SLI_ALLREDUCE_FUSED_WG);
+    }
+    // region: 0 for wo, 1 for down (FUSED_WG keeps their slots and per-workgroup epochs apart)
+    static EpiPush<1> push_epi(sli_model* m, const float* rscale, int region) {
         OneShotArgs a{};
         for (int r = 0; r < m->c.tp_size; ++r) a.peers[r] = m->os_peer[r];
         a.rank = m->c.tp_rank;
@@ -678,7 +682,11 @@ struct StepRecorder {
         a.epoch = m->os_epoch;
         a.st = m->st;
         a.loopback = m->os_loopback;
-        return EpiPush<1>{m->c.tp_rank == 0 ? m->x : nullptr, rscale, 1.0f, m->D, a, m->os_epoch + 1, m->os_peer_tab};
+        EpiPush<1> e{m->c.tp_rank == 0 ? m->x : nullptr, rscale, 1.0f, m->D, a, m->os_epoch + 1, m->os_peer_tab};
+        e.wg_mode = m->ar_mode == SLI_ALLREDUCE_FUSED_WG ? 1 : 0;
+        e.region = region;
+        e.wg_epoch = m->os_wg_epoch;
+        return e;
     }
     static int oneshot(sli_model* m, const void* src, void* dst, int n, bool max_u64) {
         OneShotArgs a{};
@@ -1953,11 +1961,13 @@ int sli_model_comm_handle(sli_model* m, void* out, int32_t n) {
     SLI_HIP(hipSetDevice(m->c.device));
     if (!m->os_buf) {
         m->os_nmax = (std::max(m->B * m->D, 2 * m->B) + 3) & ~3;
-        m->os_bytes = 256 + sizeof(float) * 2 * (size_t)kOsMaxRanks * m->os_nmax;
+        m->os_bytes = os_buffer_bytes(m->os_nmax);
         SLI_HIP(hipExtMallocWithFlags((void**)&m->os_buf, m->os_bytes, hipDeviceMallocUncached));
         SLI_HIP(hipMemset(m->os_buf, 0, m->os_bytes));
         SLI_TRY(model_alloc(m, (void**)&m->os_epoch, 16 * sizeof(unsigned)));
         SLI_HIP(hipMemset(m->os_epoch, 0, 16 * sizeof(unsigned)));
+        SLI_TRY(model_alloc(m, (void**)&m->os_wg_epoch, 2 * kOsMaxWg * sizeof(unsigned)));
+        SLI_HIP(hipMemset(m->os_wg_epoch, 0, 2 * kOsMaxWg * sizeof(unsigned)));
         SLI_TRY(model_alloc(m, (void**)&m->os_peer_tab, sizeof(char*) * kOsMaxRanks));
     }
     hipIpcMemHandle_t h;
@@ -2002,10 +2012,13 @@ int sli_model_set_allreduce(sli_model* m, int32_t mode) {
         m->os_open = true;
         m->os_loopback = true;
     }
-    SLI_CHECK(mode == SLI_ALLREDUCE_RCCL || mode == SLI_ALLREDUCE_ONESHOT || mode == SLI_ALLREDUCE_FUSED, SLI_ERR_ARG,
-              "unknown all-reduce mode");
-    SLI_CHECK(mode != SLI_ALLREDUCE_FUSED || m->B == 1, SLI_ERR_STATE,
+    SLI_CHECK(mode == SLI_ALLREDUCE_RCCL || mode == SLI_ALLREDUCE_ONESHOT || mode == SLI_ALLREDUCE_FUSED ||
+                  mode == SLI_ALLREDUCE_FUSED_WG,
+              SLI_ERR_ARG, "unknown all-reduce mode");
+    SLI_CHECK((mode != SLI_ALLREDUCE_FUSED && mode != SLI_ALLREDUCE_FUSED_WG) || m->B == 1, SLI_ERR_STATE,
               "the fused all-reduce rides the batch-1 GEMV epilogues (batch > 1: oneshot or rccl)");
+    SLI_CHECK(mode != SLI_ALLREDUCE_FUSED_WG || gemv_max_blocks() <= kOsMaxWg, SLI_ERR_SHAPE,
+              "per-workgroup exchange: more GEMV workgroups than flag slots");
     SLI_CHECK(mode == SLI_ALLREDUCE_RCCL || m->os_open, SLI_ERR_STATE, "one-shot all-reduce: open the peers first");
     SLI_CHECK(mode == SLI_ALLREDUCE_RCCL || !m->os_dead, SLI_ERR_STATE,
               "one-shot all-reduce: a wait timed out earlier, the ranks' epochs may disagree");

@@ -829,7 +829,15 @@ namespace sli {
 
 constexpr int kGemvMaxCols = 16384 - kGemvLdsHead;  // x staged in 64 KiB of LDS (<= kGemvThreads*4*kGemvStageV4)
 // persistent grid: one workgroup per CU of the current device (MI355X: 8 XCDs x 32 CUs = 256)
-inline int gemv_max_blocks() { return device_cus(); }
+// one persistent workgroup per CU; SLI_DEBUG_GEMV_MAX_BLOCKS caps it (tests: rank processes sharing one GPU
+// under the per-workgroup exchange, whose grids must fit the device together)
+inline int gemv_max_blocks() {
+    static const int cap = [] {
+        const char* e = getenv("SLI_DEBUG_GEMV_MAX_BLOCKS");
+        return e ? atoi(e) : 0;
+    }();
+    return cap > 0 ? std::min(cap, device_cus()) : device_cus();
+}
 
 // Grid: enough workgroups for every (unit, column part) item to have a wave, capped at the persistent
 // size; the balanced schedule in gemv_block spreads the items over whatever grid this returns.

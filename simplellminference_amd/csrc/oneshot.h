@@ -17,6 +17,7 @@
 // identically (one thread of every call), so the captured graph replays it.
 #pragma once
 #include "common.h"
+#include "gemv.h"
 #include "step_state.h"
 
 namespace sli {
@@ -24,6 +25,12 @@ namespace sli {
 constexpr int kOsMaxRanks = 8;
 constexpr unsigned kOsSpinLimit = 1u << 24;  // bounded wait (~seconds): gives up with DevState::error bit 4
 constexpr int kOsErrTimeout = 4;
+// Per-workgroup exchange (EpiPush::wg_mode): flags [region 2][par 2][kOsMaxWg][kOsMaxRanks] u32 after the 256-B
+// header of the launch-level flags, then the data blocks of 8 slots x nmax floats: launch-level par 0 / 1, then
+// region 0 (wo) par 0 / 1, region 1 (down) par 0 / 1.
+constexpr int kOsMaxWg = 512;
+constexpr size_t kOsDataOff = 256 + sizeof(unsigned) * 2 * 2 * kOsMaxWg * kOsMaxRanks;
+inline size_t os_buffer_bytes(int nmax) { return kOsDataOff + sizeof(float) * 6 * (size_t)kOsMaxRanks * nmax; }
 
 struct OneShotArgs {
     char* peers[kOsMaxRanks];  // every rank's comm buffer, mapped in this process (own one included)
@@ -42,7 +49,13 @@ __device__ __forceinline__ unsigned* os_flag(char* buf, int par, int r) {
     return reinterpret_cast<unsigned*>(buf) + par * kOsMaxRanks + r;
 }
 __device__ __forceinline__ float* os_data(char* buf, int par, int r, int nmax) {
-    return reinterpret_cast<float*>(buf + 256) + ((size_t)par * kOsMaxRanks + r) * nmax;
+    return reinterpret_cast<float*>(buf + kOsDataOff) + ((size_t)par * kOsMaxRanks + r) * nmax;
+}
+__device__ __forceinline__ unsigned* os_wg_flag(char* buf, int region, int par, int wg, int r) {
+    return reinterpret_cast<unsigned*>(buf + 256) + ((size_t)(region * 2 + par) * kOsMaxWg + wg) * kOsMaxRanks + r;
+}
+__device__ __forceinline__ float* os_wg_data(char* buf, int region, int par, int r, int nmax) {
+    return reinterpret_cast<float*>(buf + kOsDataOff) + ((size_t)(2 + region * 2 + par) * kOsMaxRanks + r) * nmax;
 }
 
 // Flags, bounded wait and the rank-order reduction of epoch e, by threads [0, nthr) of ONE workgroup
@@ -156,16 +169,27 @@ struct EpiPush {
     OneShotArgs os;      // dst = x, n = nrows (batch 1)
     unsigned* arrive;    // [9] arrival counters (8 shards + top), zero between launches (last arrivers reset)
     char* const* peer_tab;  // device copy of os.peers (the last arriver's runtime-indexed flags and slots)
+    // Per-workgroup mode (SLI_ALLREDUCE_FUSED_WG): every rank runs the same grid over the same rows, so
+    // workgroup w of every rank owns the same rows; w pushes its rows, raises flag[region][par][w][rank] on
+    // every rank, waits for the N flags of w on its own buffer and sums its rows' N slots in rank order into
+    // x. No launch-wide arrival and no single summing workgroup; each workgroup keeps its own epoch
+    // (wg_epoch[region][w]). Every workgroup waits, so the ranks must not share a device (or their grids must
+    // fit it together: SLI_DEBUG_GEMV_MAX_BLOCKS in the one-GPU tests).
+    int wg_mode = 0;
+    int region = 0;              // 0: wo, 1: down (their grids map rows to workgroups differently)
+    unsigned* wg_epoch = nullptr;  // [2][kOsMaxWg]
     unsigned e = 0;
     int pre_u = -1;
     float pre_r[R] = {}, pre_s[R] = {};
+    int st_u0 = -1, st_n = 0;  // wg_mode: the units this thread stored (u0, u0 + 1024, ...)
     __device__ int units() const { return (nrows + R - 1) / R; }
     __device__ void rows(int u, int* r) const {
 #pragma unroll
         for (int i = 0; i < R; ++i) r[i] = min(u * R + i, nrows - 1);
     }
     __device__ void prefetch_a(int u) {
-        e = *os.epoch + 1;  // written by the previous all-reduce's last arriver (an earlier launch)
+        // written by the previous all-reduce's last arriver / this workgroup index's previous exchange (earlier launches)
+        e = (wg_mode ? wg_epoch[region * kOsMaxWg + blockIdx.x] : *os.epoch) + 1;
         pre_u = u;
         const float* rp = resid ? resid : rscale ? rscale : os.dst;
         const float* sp = rscale ? rscale : os.dst;
@@ -177,9 +201,11 @@ struct EpiPush {
         }
     }
     __device__ void prefetch_b(int) {}
-    __device__ void store(int u, const int*, const float* v) const {
+    __device__ void store(int u, const int*, const float* v) {
         const bool pre = u == pre_u;
         const int par = (int)(e & 1u);
+        if (st_u0 < 0) st_u0 = u;
+        ++st_n;
 #pragma unroll
         for (int i = 0; i < R; ++i) {
             const int row = u * R + i;
@@ -189,14 +215,60 @@ struct EpiPush {
                 if (resid) a = (pre ? pre_r[i] : resid[row]) + a;  // add_kernel.cpp:5-14, once (rank 0)
 #pragma unroll
                 for (int p = 0; p < kOsMaxRanks; ++p)
-                    if (p < os.nranks) os_data(os.peers[p], par, os.rank, os.nmax)[row] = a;
+                    if (p < os.nranks)
+                        (wg_mode ? os_wg_data(os.peers[p], region, par, os.rank, os.nmax)
+                                 : os_data(os.peers[p], par, os.rank, os.nmax))[row] = a;
             }
         }
+    }
+    // wg_mode: flags, bounded wait and the rank-order sum of this workgroup's own rows
+    __device__ void finish_wg(int* sh) const {
+        const int tid = threadIdx.x, par = (int)(e & 1u);
+        if (tid < os.nranks)
+            __hip_atomic_store(os_wg_flag(peer_tab[tid], region, par, blockIdx.x, os.loopback ? tid : os.rank), e,
+                               __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (tid == 0) sh[1] = 0;
+        __syncthreads();
+        if (tid < os.nranks) {
+            const unsigned* f = os_wg_flag(peer_tab[os.rank], region, par, blockIdx.x, tid);
+            for (unsigned spins = 0; __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != e; ++spins) {
+                if (spins >= kOsSpinLimit) {
+                    __hip_atomic_fetch_or(&os.st->error, kOsErrTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    sh[1] = 1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        __syncthreads();
+        char* mine = peer_tab[os.rank];
+        for (int k = 0; k < st_n; ++k) {
+            const int u = st_u0 + k * kGemvThreads;
+#pragma unroll
+            for (int i = 0; i < R; ++i) {
+                const int row = u * R + i;
+                if (row >= nrows) continue;
+                float v[kOsMaxRanks];  // every rank's slot in flight at once, then summed in rank order
+#pragma unroll
+                for (int r = 0; r < kOsMaxRanks; ++r)
+                    v[r] = os_wg_data(mine, region, par, min(r, os.nranks - 1), os.nmax)[row];
+                float acc = v[0];
+#pragma unroll
+                for (int r = 1; r < kOsMaxRanks; ++r)
+                    if (r < os.nranks) acc += v[r];
+                os.dst[row] = sh[1] ? __builtin_nanf("") : acc;  // a timed-out wait: loud, not stale
+            }
+        }
+        if (tid == 0) wg_epoch[region * kOsMaxWg + blockIdx.x] = e;
     }
     __device__ void finish(float* smem) const {
         int* sh = reinterpret_cast<int*>(smem) + 40;  // [0]: last arriver, [1]: abort (gemv LDS head)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every pushing wave drains before the arrival
         __syncthreads();
+        if (wg_mode) {
+            finish_wg(sh);
+            return;
+        }
         if (threadIdx.x == 0) {  // two-level arrival: a shard per blockIdx % 8 (an XCD under round-robin
                                  // placement: speed only), then the shards' last arrivers on arrive[8]
             const unsigned g = gridDim.x, sd = blockIdx.x & 7u;

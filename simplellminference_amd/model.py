@@ -186,9 +186,10 @@ class LlamaModel:
         return self
 
     def set_allreduce(self, mode: str) -> "LlamaModel":
-        """"rccl" (ncclAllReduce in the step graph), "oneshot" (oneshot.h, after comm_open) or "fused" (the
-        one-shot exchange inside the wo / down GEMV launches, batch 1; oneshot.h EpiPush)."""
-        call("sli_model_set_allreduce", self._h, {"rccl": 0, "oneshot": 1, "fused": 2}[mode])
+        """"rccl" (ncclAllReduce in the step graph), "oneshot" (oneshot.h, after comm_open), "fused" (the
+        one-shot exchange inside the wo / down GEMV launches, batch 1; oneshot.h EpiPush) or "fused_wg" (the
+        same per workgroup: ranks on distinct devices, sli.h SLI_ALLREDUCE_FUSED_WG)."""
+        call("sli_model_set_allreduce", self._h, {"rccl": 0, "oneshot": 1, "fused": 2, "fused_wg": 3}[mode])
         return self
 
     # ------------------------------------------------------------------ model.cpp:40-140

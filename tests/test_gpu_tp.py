@@ -133,9 +133,18 @@ def test_tp_rank_of_c2_shapes_steps_nocomm(gpu, monkeypatch, w, world):
 LONG_PROMPT = [(7 * i + 3) % 500 for i in range(23)]
 
 
+def _preset(name):
+    """"llama2-7b:2" = the preset cut to 2 layers (full-size shard shapes in a test-sized step)."""
+    from simplellminference_amd.model import preset
+    base, _, layers = name.partition(":")
+    return preset(base, num_hidden_layers=int(layers)) if layers else preset(base)
+
+
 def _oneshot_rank(rank, world, port, name, batch, q, mode="oneshot", w="f16", prefill=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0",
                       SLI_DEBUG_NOCOMM="1")  # no RCCL communicator: the one-shot kernels are the only exchange
+    if mode == "fused_wg":  # every workgroup waits for its peers': the ranks' grids must fit the one GPU together
+        os.environ["SLI_DEBUG_GEMV_MAX_BLOCKS"] = str(256 // (2 * world))
     import torch
     import torch.distributed as dist
 
@@ -144,7 +153,7 @@ def _oneshot_rank(rank, world, port, name, batch, q, mode="oneshot", w="f16", pr
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         dev = rank % torch.cuda.device_count()
-        m = LlamaModel(config=preset(name), w_dtype=w, kv_dtype="f16", tp_rank=rank, tp_size=world,
+        m = LlamaModel(config=_preset(name), w_dtype=w, kv_dtype="f16", tp_rank=rank, tp_size=world,
                        device=dev, seed=0, batch=batch).init()
         tp.open_oneshot(m)
         m.set_allreduce(mode)
@@ -169,13 +178,16 @@ def _oneshot_rank(rank, world, port, name, batch, q, mode="oneshot", w="f16", pr
 
 
 @pytest.mark.parametrize("name,batch,mode", [("tiny", 1, "oneshot"), ("tiny-gqa", 1, "oneshot"), ("tiny-gqa", 2, "oneshot"),
-                                             ("tiny", 1, "fused"), ("tiny-gqa", 1, "fused"), ("tiny-h8", 1, "fused")])
+                                             ("tiny", 1, "fused"), ("tiny-gqa", 1, "fused"), ("tiny-h8", 1, "fused"),
+                                             ("tiny", 1, "fused_wg"), ("tiny-gqa", 1, "fused_wg"),
+                                             ("tiny-h8", 1, "fused_wg")])
 def test_oneshot_allreduce_two_processes(gpu, name, batch, mode):
     """The one-shot all-reduce (oneshot.h) between two rank PROCESSES through IPC-mapped uncached buffers
     (both on device 0 here; on the 8-GPU node each on its own GPU, over xGMI): greedy tokens identical to
     the TP = 1 engine, logits within 1e-3, no device error (the bounded waits never gave up). mode "fused":
     the exchange runs inside the wo / down GEMV launches (EpiPush: rows pushed from the epilogue, the
-    launch's last workgroup waits and sums)."""
+    launch's last workgroup waits and sums); "fused_wg": per workgroup (each waits for the same workgroup of
+    the peer and sums its own rows; the grids capped so both ranks' launches fit the one GPU together)."""
     from simplellminference_amd.model import LlamaModel, preset
     ref = LlamaModel(config=preset(name), w_dtype="f16", kv_dtype="f16", seed=0, batch=batch).init()
     if batch == 1:
@@ -229,12 +241,16 @@ def test_oneshot_prefill_two_processes(gpu, mode):
 
 
 @pytest.mark.parametrize("name,world,mode,w", [("tiny-h8", 4, "fused", "f16"), ("tiny-h8", 4, "oneshot", "f16"),
-                                               ("tiny-gqa", 2, "fused", "i8")])
+                                               ("tiny-gqa", 2, "fused", "i8"), ("tiny-h8", 4, "fused_wg", "f16"),
+                                               ("tiny-gqa", 2, "fused_wg", "i8"), ("llama2-7b:2", 2, "fused_wg", "f16"),
+                                               ("llama2-7b:2", 2, "fused", "f16")])
 def test_oneshot_allreduce_more_ranks(gpu, name, world, mode, w):
-    """The one-shot exchange (separate launch or fused into wo / down) between 4 rank processes on one GPU, and
-    the fused form with int8 weights: tokens identical to the TP = 1 engine, logits within 1e-3, no device error."""
-    from simplellminference_amd.model import LlamaModel, preset
-    ref = LlamaModel(config=preset(name), w_dtype=w, kv_dtype="f16", seed=0).init()
+    """The one-shot exchange (separate launch or fused into wo / down) between 4 rank processes on one GPU, the
+    fused forms with int8 weights, and both fused forms at Llama-2-7B shard shapes (2 layers, TP 2: 64 / 256
+    workgroups per wo / down launch): tokens identical to the TP = 1 engine, logits within 1e-3, no device
+    error."""
+    from simplellminference_amd.model import LlamaModel
+    ref = LlamaModel(config=_preset(name), w_dtype=w, kv_dtype="f16", seed=0).init()
     rtoks, rlogits = ref.predict(PROMPT, 16, want_logits=True)
     ref.close()
     ctx = mp.get_context("spawn")

@@ -43,8 +43,8 @@ res[key] = {
     "all_weight_kernels_mean_hbm_bytes_per_launch": round(2 * kb * 1024),
     "all_weight_kernels_mean_fetch_size_kib_raw": round(kb, 1),
     "correction": ("x2: gfx950 FETCH_SIZE counts half the bytes of a coalesced 16-B/lane stream"
-                   + ("" if "bgemm" not in "".join(per) else "; bgemm's 16-row x 64-B fragment loads are "
-                      "not calibrated against that rule")),
+                   + ("" if "bgemm" not in "".join(per) else "; bgemm streams its weights in the fragment layout "
+                      "(one contiguous KiB per wave load), the same coalesced 16-B/lane pattern")),
     "dominant_family": dom,
     "dominant_family_algorithmic_bytes_per_launch": round(alg),
     "weight_kernel_dispatches": len(gemv),
