@@ -855,8 +855,7 @@ struct StepRecorder {
             SLI_TRY(record_phase(m, p));
             SLI_TRY(allreduce_x(m));
         }
-        if (m->ar_mode == SLI_ALLREDUCE_ONESHOT || m->ar_mode == SLI_ALLREDUCE_FUSED) {  // the argmax keys through
-                                                                                          // the one-shot exchange
+        if (m->ar_mode != SLI_ALLREDUCE_RCCL) {  // the argmax keys through the one-shot exchange
             SLI_TRY(record_head(m, true));
             void* k = m->B > 1 ? (void*)m->bkeys : (void*)&m->st->key;
             SLI_TRY(oneshot(m, k, k, 2 * m->B, true));

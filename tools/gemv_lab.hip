@@ -410,6 +410,80 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
+    if (mode == "wo") {
+        // the batch-1 wo launches at C1 (Llama-2-7B, 32 heads x 8 splits of 256 positions at position 2047):
+        // plain input, merge-staged (ks 1) and the K-split merge-staged form (ks 2, the engine's default), with
+        // per-wave phase stamps beside the streaming-read floor of the same bytes
+        const int D = 4096, H = 32, HD = 128, MS = 8, PS = HD + 2;  // kAttnPartPad = 2
+        float* part;
+        int32_t* posd;
+        CK(hipMalloc(&part, sizeof(float) * H * MS * PS));
+        CK(hipMalloc(&posd, 64));
+        hipLaunchKernelGGL(fill_f, dim3(64), dim3(256), 0, s, part, (size_t)H * MS * PS, 13u);
+        const int32_t pos = 2047;
+        CK(hipMemcpy(posd, &pos, 4, hipMemcpyHostToDevice));
+        float* kp;
+        CK(hipMalloc(&kp, sizeof(float) * 4 * D));
+        const int nst = 256 * 16 * 4;
+        unsigned long long* st;
+        CK(hipMalloc(&st, (size_t)NL * nst * 8));
+        std::vector<unsigned long long> h((size_t)NL * nst);
+        const long long bytes = (long long)D * D * 2;
+        auto run = [&](int variant, int l, unsigned long long* stp) {
+            GemvIn in{x, nullptr, 0.0f, D};
+            in.stamps = stp;
+            AttnMergeIn am{part, posd, MS, 256, HD};
+            if (variant == 0) {
+                EpiStore<1> e{y, nullptr, nullptr, 1.0f, D};
+                CK((launch_gemv_u<__half, 1, 2, true>(w[1][l], in, e, D, s)));
+            } else if (variant == 1) {
+                EpiStore<1> e{y, nullptr, nullptr, 1.0f, D};
+                GemvIn im{nullptr, nullptr, 0.0f, D};
+                im.stamps = stp;
+                CK((launch_gemv_merge<__half, 1, 2, true>(w[1][l], im, e, am, D, s)));
+            } else {
+                const int ks = 2;
+                GemvIn im{nullptr, nullptr, 0.0f, D / ks};
+                im.stamps = stp;
+                am.ksplit = ks;
+                am.kunits = D;
+                const EpiKPart e{kp, nullptr, D, ks};
+                CK((launch_gemv_merge_ks<__half, 1, 2, true, EpiKPart, 8, 4>(w[1][l], im, e, am, gemv_ksplit_grid(D, ks), s)));
+            }
+        };
+        const float s_ms = time_graph(s, [&] {
+            for (int l = 0; l < NL; ++l)
+                hipLaunchKernelGGL(stream_kernel<8>, dim3(256), dim3(1024), 0, s, (const char*)w[1][l], bytes, y2, nullptr);
+        });
+        const char* names[] = {"wo plain", "wo merge ks1", "wo merge ks2"};
+        for (int v = 0; v < 3; ++v) {
+            const float g_ms = time_graph(s, [&] { for (int l = 0; l < NL; ++l) run(v, l, nullptr); });
+            CK(hipMemset(st, 0, (size_t)NL * nst * 8));
+            time_graph(s, [&] { for (int l = 0; l < NL; ++l) run(v, l, st + (size_t)l * nst); }, 1);
+            CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+            std::vector<double> ent, stg, ex;
+            for (int l = 2; l < NL; ++l) {
+                const unsigned long long* q = h.data() + (size_t)l * nst;
+                unsigned long long t0 = ~0ull;
+                for (int i = 0; i < 4096; ++i)
+                    if (q[i * 4 + 3]) t0 = std::min(t0, q[i * 4]);
+                for (int i = 0; i < 4096; ++i) {
+                    if (q[i * 4 + 3] == 0) continue;
+                    ent.push_back((q[i * 4] - t0) * 0.01);
+                    stg.push_back((q[i * 4 + 1] - t0) * 0.01);
+                    ex.push_back((q[i * 4 + 2] - t0) * 0.01);
+                }
+            }
+            std::sort(ent.begin(), ent.end());
+            std::sort(stg.begin(), stg.end());
+            std::sort(ex.begin(), ex.end());
+            auto pc = [](std::vector<double>& vv, double f) { return vv.empty() ? 0.0 : vv[(size_t)(f * (vv.size() - 1))]; };
+            printf("%-13s gemv %6.2f us  stream %6.2f us | entry p50 %5.2f max %5.2f | staged p50 %5.2f p99 %5.2f | "
+                   "exit p10 %5.2f p50 %5.2f p90 %5.2f max %5.2f\n", names[v], 1000.0 * g_ms / NL, 1000.0 * s_ms / NL,
+                   pc(ent, .5), pc(ent, 1.0), pc(stg, .5), pc(stg, .99), pc(ex, .1), pc(ex, .5), pc(ex, .9), pc(ex, 1.0));
+        }
+        return 0;
+    }
     if (mode == "tp8") {
         // the TP-8 shard GEMVs as the engine launches them (launch_gemv_u: the column split at these sizes), per
         // launch phase stamps, beside the streaming-read floor of the same bytes: where a small launch's time goes
