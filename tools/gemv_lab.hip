@@ -441,7 +441,7 @@ int main(int argc, char** argv) {
                 GemvIn im{nullptr, nullptr, 0.0f, D};
                 im.stamps = stp;
                 CK((launch_gemv_merge<__half, 1, 2, true>(w[1][l], im, e, am, D, s)));
-            } else {
+            } else if (variant == 2) {
                 const int ks = 2;
                 GemvIn im{nullptr, nullptr, 0.0f, D / ks};
                 im.stamps = stp;
@@ -449,14 +449,31 @@ int main(int argc, char** argv) {
                 am.kunits = D;
                 const EpiKPart e{kp, nullptr, D, ks};
                 CK((launch_gemv_merge_ks<__half, 1, 2, true, EpiKPart, 8, 4>(w[1][l], im, e, am, gemv_ksplit_grid(D, ks), s)));
+            } else if (variant == 3) {  // int8 (the fp16 buffer reinterpreted: half its bytes), plain input
+                EpiStore<1> e{y, nullptr, nullptr, 1.0f, D};
+                CK((launch_gemv_u<int8_t, 1, 2, true>((const int8_t*)w[1][l], in, e, D, s)));
+            } else {  // int8 K-split merge-staged (the engine's C3 wo)
+                const int ks = 2;
+                GemvIn im{nullptr, nullptr, 0.0f, D / ks};
+                im.stamps = stp;
+                am.ksplit = ks;
+                am.kunits = D;
+                const EpiKPart e{kp, nullptr, D, ks};
+                CK((launch_gemv_merge_ks<int8_t, 1, 1, true, EpiKPart, 8, 2>((const int8_t*)w[1][l], im, e, am,
+                                                                             gemv_ksplit_grid(D, ks), s)));
             }
         };
         const float s_ms = time_graph(s, [&] {
             for (int l = 0; l < NL; ++l)
                 hipLaunchKernelGGL(stream_kernel<8>, dim3(256), dim3(1024), 0, s, (const char*)w[1][l], bytes, y2, nullptr);
         });
-        const char* names[] = {"wo plain", "wo merge ks1", "wo merge ks2"};
-        for (int v = 0; v < 3; ++v) {
+        const char* names[] = {"wo plain", "wo merge ks1", "wo merge ks2", "i8 wo plain", "i8 wo merge ks2"};
+        const float s8_ms = time_graph(s, [&] {
+            for (int l = 0; l < NL; ++l)
+                hipLaunchKernelGGL(stream_kernel<8>, dim3(256), dim3(1024), 0, s, (const char*)w[1][l], bytes / 2, y2, nullptr);
+        });
+        for (int v = 0; v < 5; ++v) {
+            const float sv_ms = v >= 3 ? s8_ms : s_ms;
             const float g_ms = time_graph(s, [&] { for (int l = 0; l < NL; ++l) run(v, l, nullptr); });
             CK(hipMemset(st, 0, (size_t)NL * nst * 8));
             time_graph(s, [&] { for (int l = 0; l < NL; ++l) run(v, l, st + (size_t)l * nst); }, 1);
@@ -479,7 +496,7 @@ int main(int argc, char** argv) {
             std::sort(ex.begin(), ex.end());
             auto pc = [](std::vector<double>& vv, double f) { return vv.empty() ? 0.0 : vv[(size_t)(f * (vv.size() - 1))]; };
             printf("%-13s gemv %6.2f us  stream %6.2f us | entry p50 %5.2f max %5.2f | staged p50 %5.2f p99 %5.2f | "
-                   "exit p10 %5.2f p50 %5.2f p90 %5.2f max %5.2f\n", names[v], 1000.0 * g_ms / NL, 1000.0 * s_ms / NL,
+                   "exit p10 %5.2f p50 %5.2f p90 %5.2f max %5.2f\n", names[v], 1000.0 * g_ms / NL, 1000.0 * sv_ms / NL,
                    pc(ent, .5), pc(ent, 1.0), pc(stg, .5), pc(stg, .99), pc(ex, .1), pc(ex, .5), pc(ex, .9), pc(ex, 1.0));
         }
         return 0;
