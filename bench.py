@@ -48,13 +48,10 @@ FAMILY_KERNELS = {
             "gate_up": "gemv_sum_kernel<EpiSwiGLU> (residual + wo partials staged, RMSNorm + [gate;up] GEMV + "
                        "sigmoid(g)*u)",
             "down": "gemv_kernel<EpiStoreSum> (down GEMV + residual + wo partials -> x)",
-            "lm_head": "gemv_kernel<EpiLogits> (RMSNorm + tied LM head + argmax keys; in the step its last "
-                       "workgroup reduces the keys and updates the decode state)"},
+            "lm_head": "gemv_kernel<EpiLogits> (RMSNorm + tied LM head + argmax keys)"},
     True: {"qkv": "bgemm_kernel<BgEpiQKV> (MFMA 16x16x32 f16)", "attention": "attn_partial_kernel (batched kv heads)",
            "wo": "bgemm_kernel<BgEpiStore> (MFMA)", "gate_up": "bgemm_kernel<BgEpiSwiGLU> (MFMA)",
-           "down": "bgemm_kernel<BgEpiStore> (MFMA)",
-           "lm_head": "bgemm_kernel<BgEpiLogits> (MFMA; in the step its last group reduces the keys and updates "
-                      "every sequence's state)"},
+           "down": "bgemm_kernel<BgEpiStore> (MFMA)", "lm_head": "bgemm_kernel<BgEpiLogits> (MFMA)"},
 }
 
 

@@ -23,7 +23,6 @@
 //     attention.h, MI355X_MICROARCH.md).
 #pragma once
 #include "common.h"
-#include "step_state.h"
 
 namespace sli {
 
@@ -494,15 +493,6 @@ struct BgEpiLogits {
     float* logits;                 // [B][ld]
     unsigned long long* keys_out;  // [B][key_ld]
     int nrows, ld, vocab_off, key_ld;
-    // fin set (no key exchange): the last group to finish also reduces every group's keys per sequence and
-    // updates each sequence's state (keyreduce_batch_kernel + finalize_batch_kernel folded in): keys stored
-    // write-through (sc1) and drained, one agent-scope arrival per group, sc1 loads by the last arriver
-    unsigned* fin = nullptr;       // arrival counter, zero between launches (the last arriver resets it)
-    int ngroups = 0;
-    DevState* st = nullptr;        // [B]
-    const int32_t* prompt = nullptr;  // [B][T + 1]
-    int32_t* hist = nullptr;          // [B][T + 1]
-    int T = 0;
     __device__ int row(int t, int i) const { return min(t * 16 + i, nrows - 1); }
     __device__ void one(int row, int b, float v, unsigned long long* kl) const {
         if (row >= nrows) return;
@@ -515,37 +505,7 @@ struct BgEpiLogits {
     }
     __device__ void finish(unsigned long long* kl, int g, int B) const {
         __syncthreads();
-        if (!fin) {
-            if ((int)threadIdx.x < B) keys_out[(size_t)threadIdx.x * key_ld + g] = kl[threadIdx.x];
-            return;
-        }
-        if ((int)threadIdx.x < B)
-            __hip_atomic_store(keys_out + (size_t)threadIdx.x * key_ld + g, kl[threadIdx.x], __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every key drains before the arrival
-        __syncthreads();
-        int* last = reinterpret_cast<int*>(kl + 10);  // scratch past the keys and the split flag
-        if (threadIdx.x == 0) {
-            const unsigned prev = __hip_atomic_fetch_add(fin, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            *last = prev == (unsigned)(ngroups - 1);
-            if (*last) __hip_atomic_store(fin, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __syncthreads();
-        if (!*last) return;  // uniform
-        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-        if (wave < B) {  // wave b: sequence b's keys over every group, then its state (model.cpp:157-183)
-            unsigned long long b = 0;
-            for (int i = lane; i < ngroups; i += 64) {
-                const unsigned long long k =
-                    __hip_atomic_load(keys_out + (size_t)wave * key_ld + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                b = k > b ? k : b;
-            }
-            b = wave_max_u64(b);
-            if (lane == 0) {
-                st[wave].key = b;
-                finalize_state(st + wave, prompt + (size_t)wave * (T + 1), hist + (size_t)wave * (T + 1), T);
-            }
-        }
+        if ((int)threadIdx.x < B) keys_out[(size_t)threadIdx.x * key_ld + g] = kl[threadIdx.x];
     }
 };
 

@@ -95,7 +95,6 @@ struct sli_model {
     sli::BgPlan bp_qkv, bp_wo, bp_gu, bp_down, bp_lm;
     float* bg_ws = nullptr;               // split-K partials of the batched projections
     unsigned* bg_cnt = nullptr;           // their arrival counters (zero between launches)
-    unsigned* lm_fin = nullptr;           // batch-1 LM head's arrival counter (EpiLogits::fin), zero between launches
     unsigned long long* bkeys = nullptr;  // [B] per-sequence argmax keys (all-reduced MAX under TP)
     int key_ld = 0;                       // per-sequence stride of the per-workgroup argmax keys
     // prompt prefill (sli_model_prefill, prefill.h): chunks of up to kPfMaxChunk prompt positions through
@@ -526,15 +525,6 @@ __global__ void group_finalize_kernel(GroupKeyArgs a) {
 
 // batched decode: the attention's split merge as its own launch (attention.h attn_merge_kernel, mode 2);
 // SLI_ATTN_MERGE_LAUNCH=0 keeps the last-arriver merge inside the attention launch (A/B measurement)
-// SLI_LM_FINALIZE=0: the batch-1 step ends with a separate key-reduce launch (A/B measurement)
-static bool lm_finalize() {
-    static const bool v = [] {
-        const char* e = getenv("SLI_LM_FINALIZE");
-        return !(e && e[0] == '0');
-    }();
-    return v;
-}
-
 static int defer_batched() {
     static const int v = [] {
         const char* e = getenv("SLI_ATTN_MERGE_LAUNCH");
@@ -668,18 +658,9 @@ struct StepRecorder {
         const int cs = gemv_split<WT, 4>(units, m->D).cs;
         return cs == 1 ? gemv_balanced_blocks(units) : gemv_blocks(units, cs);  // launch_gemv's grid
     }
-    // finalize: the launch's last workgroup also reduces the keys and updates the state (the step's tail;
-    // the timing probes pass false, so they never advance the state)
-    static int gemv_lm(sli_model* m, bool finalize = false) {
+    static int gemv_lm(sli_model* m) {
         GemvIn in{m->x, m->norms + (size_t)(2 * m->L) * m->D, m->c.eps, m->D};
         EpiLogits<2> e{m->logits, m->keys, m->emb_s ? m->emb_s + m->v_lo : nullptr, m->v_n, m->v_lo, 0ull};
-        if (finalize) {
-            e.fin = m->lm_fin;
-            e.st = m->st;
-            e.prompt = m->prompt;
-            e.hist = m->hist;
-            e.T = m->T;
-        }
         const WT* w = (const WT*)m->emb + (size_t)m->v_lo * m->D;
         SLI_HIP((launch_gemv_u<WT, 2, 4, NT>(w, in, e, (m->v_n + 1) / 2, m->stream)));
         return SLI_OK;
@@ -793,16 +774,8 @@ struct StepRecorder {
         BgEpiStore e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, nullptr, 1.0f, m->D, m->D};
         return bg(m, m->bg_tiled ? m->layers[l].down_t : m->layers[l].down, bin(m, m->act, nullptr, m->Il), e, m->bp_down);
     }
-    static int b_lm(sli_model* m, bool finalize = false) {
+    static int b_lm(sli_model* m) {
         BgEpiLogits e{m->logits, m->keys, m->v_n, m->v_n, m->v_lo, m->key_ld};
-        if (finalize) {  // the step's tail in the launch's last group (timing probes pass false)
-            e.fin = m->lm_fin;
-            e.ngroups = m->bp_lm.groups;
-            e.st = m->st;
-            e.prompt = m->prompt;
-            e.hist = m->hist;
-            e.T = m->T;
-        }
         const void* w = m->bg_tiled ? m->lm_t : wptr(m->emb, m->wbytes, (size_t)m->v_lo * m->D);
         return bg(m, w, bin(m, m->x, m->norms + (size_t)(2 * m->L) * m->D, m->D), e, m->bp_lm);
     }
@@ -850,7 +823,6 @@ struct StepRecorder {
             SLI_HIP(hipGetLastError());
             return SLI_OK;
         }
-        if (!exchange && lm_finalize()) return gemv_lm(m, true);  // key reduce + state update in its last workgroup
         SLI_TRY(gemv_lm(m));
         if (exchange)
             hipLaunchKernelGGL(keyreduce_kernel<false>, dim3(1), dim3(kKeyThreads), 0, s, m->keys, lm_head_blocks(m),
@@ -890,7 +862,6 @@ struct StepRecorder {
             return record_finalize(m);
         }
         if (!m->collectives) {
-            if (m->B > 1 && lm_finalize()) return b_lm(m, true);  // keys reduced + states updated in its last group
             SLI_TRY(record_head(m, m->B > 1));
             return m->B > 1 ? record_finalize(m) : SLI_OK;
         }
@@ -1414,7 +1385,6 @@ static int create_model(const sli_model_config* cfg, const void* comm_id, sli_tp
         A((void**)&m->bg_cnt, sizeof(unsigned) * bg_groups);
     }
     A((void**)&m->bkeys, sizeof(unsigned long long) * B);
-    A((void**)&m->lm_fin, 64);
 
     A((void**)&m->sin_t, sizeof(float) * (size_t)m->T * (hd / 2));
     A((void**)&m->cos_t, sizeof(float) * (size_t)m->T * (hd / 2));
@@ -1430,7 +1400,6 @@ static int create_model(const sli_model_config* cfg, const void* comm_id, sli_tp
         hipMemcpy(m->cos_t, co.data(), co.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
         return bail(fail(SLI_ERR_HIP, "rope table upload"));
     if (hipMemset(m->prompt, 0, sizeof(int32_t) * B * (m->T + 1)) != hipSuccess ||
-        hipMemset(m->lm_fin, 0, 64) != hipSuccess ||
         hipMemset(m->attn_count, 0, sizeof(unsigned) * B * m->hkv) != hipSuccess ||
         hipMemset(m->hist, 0, sizeof(int32_t) * B * (m->T + 1)) != hipSuccess ||
         (m->bg_cnt && hipMemset(m->bg_cnt, 0, sizeof(unsigned) * bg_groups) != hipSuccess))

@@ -15,7 +15,6 @@
 #include <type_traits>
 
 #include "common.h"
-#include "step_state.h"
 
 namespace sli {
 
@@ -773,10 +772,7 @@ struct EpiSwiGLU {
 
 // LM head (model.cpp:136-139, tied to the embedding) + first stage of the device argmax: logits are
 // stored and each workgroup writes the max orderable key of the rows it owned to keys[blockIdx.x]
-// (deterministic two-stage reduction; no atomics on one word). With fin set (batch 1, no key exchange) the
-// launch's last workgroup also runs the second stage and the state update (keyreduce_kernel<true> folded in):
-// keys stored write-through (sc1) and drained, one agent-scope arrival per workgroup, the last arriver reads
-// every key with sc1 loads (MI355X_MICROARCH.md hand-off row 1) and finalizes.
+// (deterministic two-stage reduction; no atomics on one word).
 template <int R>
 struct EpiLogits {
     float* logits;
@@ -787,11 +783,6 @@ struct EpiLogits {
     unsigned long long best;
     int pre_u = -1;
     float pre_s[R] = {};
-    unsigned* fin = nullptr;  // arrival counter (zero between launches; the last arriver resets it)
-    DevState* st = nullptr;
-    const int32_t* prompt = nullptr;
-    int32_t* hist = nullptr;
-    int T = 0;
     __device__ int units() const { return (nrows + R - 1) / R; }
     __device__ void rows(int u, int* r) const {
 #pragma unroll
@@ -827,34 +818,7 @@ struct EpiLogits {
         if (threadIdx.x == 0) {
             unsigned long long b = 0;
             for (int w = 0; w < (kGemvThreads >> 6); ++w) b = red[w] > b ? red[w] : b;
-            if (!fin) {
-                keys[blockIdx.x] = b;
-            } else {
-                __hip_atomic_store(keys + blockIdx.x, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the key drains before the arrival
-                const unsigned prev = __hip_atomic_fetch_add(fin, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const int last = prev == gridDim.x - 1u;
-                if (last) __hip_atomic_store(fin, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                reinterpret_cast<int*>(red)[2 * (kGemvThreads >> 6)] = last;
-            }
-        }
-        if (!fin) return;
-        __syncthreads();
-        if (!reinterpret_cast<int*>(red)[2 * (kGemvThreads >> 6)]) return;  // uniform
-        unsigned long long b = 0;  // keyreduce_kernel's second stage over every workgroup's key
-        for (int i = threadIdx.x; i < (int)gridDim.x; i += kGemvThreads) {
-            const unsigned long long k = __hip_atomic_load(keys + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            b = k > b ? k : b;
-        }
-        b = wave_max_u64(b);
-        __syncthreads();
-        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = b;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned long long t = 0;
-            for (int w = 0; w < (kGemvThreads >> 6); ++w) t = red[w] > t ? red[w] : t;
-            st->key = t;
-            finalize_state(st, prompt, hist, T);  // model.cpp:157-183
+            keys[blockIdx.x] = b;
         }
     }
 };
