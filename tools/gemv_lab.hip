@@ -410,6 +410,69 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
+    if (mode == "i8s") {
+        // int8 weights (the fp16 buffers reinterpreted: half their bytes) at the C3 shapes, the engine's
+        // configurations and NB / U variants, with per-wave phase stamps beside the streaming-read floor
+        const int nst = 256 * 16 * 4;
+        unsigned long long* st;
+        CK(hipMalloc(&st, (size_t)NL * nst * 8));
+        std::vector<unsigned long long> h((size_t)NL * nst);
+        using Run = std::function<void(int, unsigned long long*)>;
+        auto report = [&](const char* name, long long bytes, int si, const Run& run) {
+            const float g_ms = time_graph(s, [&] { for (int l = 0; l < NL; ++l) run(l, nullptr); });
+            const float s_ms = time_graph(s, [&] {
+                for (int l = 0; l < NL; ++l)
+                    hipLaunchKernelGGL(stream_kernel<8>, dim3(256), dim3(1024), 0, s, (const char*)w[si][l], bytes, y2,
+                                       nullptr);
+            });
+            CK(hipMemset(st, 0, (size_t)NL * nst * 8));
+            time_graph(s, [&] { for (int l = 0; l < NL; ++l) run(l, st + (size_t)l * nst); }, 1);
+            CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+            std::vector<double> stg, ex;
+            for (int l = 2; l < NL; ++l) {
+                const unsigned long long* q = h.data() + (size_t)l * nst;
+                unsigned long long t0 = ~0ull;
+                for (int i = 0; i < 4096; ++i)
+                    if (q[i * 4 + 3]) t0 = std::min(t0, q[i * 4]);
+                for (int i = 0; i < 4096; ++i) {
+                    if (q[i * 4 + 3] == 0) continue;
+                    stg.push_back((q[i * 4 + 1] - t0) * 0.01);
+                    ex.push_back((q[i * 4 + 2] - t0) * 0.01);
+                }
+            }
+            std::sort(stg.begin(), stg.end());
+            std::sort(ex.begin(), ex.end());
+            auto pc = [](std::vector<double>& vv, double f) { return vv.empty() ? 0.0 : vv[(size_t)(f * (vv.size() - 1))]; };
+            printf("%-22s gemv %6.2f us  stream %6.2f us | staged p50 %5.2f p99 %5.2f | exit p10 %5.2f p50 %5.2f "
+                   "p90 %5.2f max %5.2f\n", name, 1000.0 * g_ms / NL, 1000.0 * s_ms / NL, pc(stg, .5), pc(stg, .99),
+                   pc(ex, .1), pc(ex, .5), pc(ex, .9), pc(ex, 1.0));
+        };
+        auto in_of = [&](int si, bool norm, unsigned long long* stp) {
+            GemvIn in{x, norm ? nw : nullptr, 1e-5f, kShapes[si].cols};
+            in.stamps = stp;
+            return in;
+        };
+#define I8_CFG(NAME, SI, NORM, R, U, NB)                                                                    \
+        report(NAME, (long long)kShapes[SI].rows * kShapes[SI].cols, SI, [&](int l, unsigned long long* stp) { \
+            EpiStore<R> e{y, nullptr, nullptr, 1.0f, kShapes[SI].rows};                                    \
+            CK((launch_gemv<int8_t, R, U, true, EpiStore<R>, NB>((const int8_t*)w[SI][l], in_of(SI, NORM, stp), \
+                                                                 e, kShapes[SI].rows / R, s)));           \
+        })
+        I8_CFG("i8 qkv R2U2NB2", 0, true, 2, 2, 2);
+        I8_CFG("i8 qkv R2U2NB3", 0, true, 2, 2, 3);
+        I8_CFG("i8 qkv R2U2NB4", 0, true, 2, 2, 4);
+        I8_CFG("i8 qkv R2U1NB4", 0, true, 2, 1, 4);
+        I8_CFG("i8 qkv R1U2NB4", 0, true, 1, 2, 4);
+        I8_CFG("i8 qkv R1U4NB2", 0, true, 1, 4, 2);
+        I8_CFG("i8 gu R2U2NB2", 2, true, 2, 2, 2);
+        I8_CFG("i8 gu R2U2NB3", 2, true, 2, 2, 3);
+        I8_CFG("i8 down R1U4NB2", 3, false, 1, 4, 2);
+        I8_CFG("i8 down R1U4NB3", 3, false, 1, 4, 3);
+        I8_CFG("i8 down R1U2NB4", 3, false, 1, 2, 4);
+        I8_CFG("i8 down R2U2NB2", 3, false, 2, 2, 2);
+#undef I8_CFG
+        return 0;
+    }
     if (mode == "wo") {
         // the batch-1 wo launches at C1 (Llama-2-7B, 32 heads x 8 splits of 256 positions at position 2047):
         // plain input, merge-staged (ks 1) and the K-split merge-staged form (ks 2, the engine's default), with
