@@ -221,17 +221,26 @@ struct EpiPush {
             }
         }
     }
-    // wg_mode: flags, bounded wait and the rank-order sum of this workgroup's own rows
+    // wg_mode: flags, bounded wait and the rank-order sum of this workgroup's own rows. Every access to the comm
+    // buffers bypasses the caches (uncached memory), and the pushes have drained (vmcnt 0, every wave, barrier)
+    // before the flag store is issued, so the flag store / poll are relaxed: a system-scope release / acquire would
+    // add an L2 write-back / invalidate per workgroup and order nothing the uncached accesses need (loopback TP-8
+    // rank step 1.494 -> 1.339 ms, profiles/r4_tp_fused_wg_relaxed.txt). SLI_OS_WG_FENCE=1: the fenced form.
+#ifndef SLI_OS_WG_FENCE
+#define SLI_OS_WG_FENCE 0
+#endif
     __device__ void finish_wg(int* sh) const {
+        constexpr int kRel = SLI_OS_WG_FENCE ? __ATOMIC_RELEASE : __ATOMIC_RELAXED;
+        constexpr int kAcq = SLI_OS_WG_FENCE ? __ATOMIC_ACQUIRE : __ATOMIC_RELAXED;
         const int tid = threadIdx.x, par = (int)(e & 1u);
         if (tid < os.nranks)
             __hip_atomic_store(os_wg_flag(peer_tab[tid], region, par, blockIdx.x, os.loopback ? tid : os.rank), e,
-                               __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                               kRel, __HIP_MEMORY_SCOPE_SYSTEM);
         if (tid == 0) sh[1] = 0;
         __syncthreads();
         if (tid < os.nranks) {
             const unsigned* f = os_wg_flag(peer_tab[os.rank], region, par, blockIdx.x, tid);
-            for (unsigned spins = 0; __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != e; ++spins) {
+            for (unsigned spins = 0; __hip_atomic_load(f, kAcq, __HIP_MEMORY_SCOPE_SYSTEM) != e; ++spins) {
                 if (spins >= kOsSpinLimit) {
                     __hip_atomic_fetch_or(&os.st->error, kOsErrTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     sh[1] = 1;
