@@ -114,7 +114,7 @@ struct sli_model {
     bool os_open = false;
     bool os_dead = false;                    // a one-shot wait timed out: set_allreduce(ONESHOT) is refused
     unsigned* os_epoch = nullptr;            // one-shot call counter; os_epoch[1..9]: fused-launch arrivals
-    unsigned* os_wg_epoch = nullptr;         // SLI_ALLREDUCE_FUSED_WG: per-(region, workgroup) epochs [2][kOsMaxWg]
+    unsigned* os_wg_epoch = nullptr;         // per-(region, workgroup) epochs [kOsRegions][kOsMaxWg] (oneshot.h)
     int os_nmax = 0;
     bool os_loopback = false;                // debug: SLI_DEBUG_OS_LOOPBACK (oneshot.h OneShotArgs::loopback)
     char** os_peer_tab = nullptr;            // device copy of os_peer (oneshot.h EpiPush::peer_tab)
@@ -524,6 +524,15 @@ __global__ void group_finalize_kernel(GroupKeyArgs a) {
 
 
 // batched decode: the attention's split merge as its own launch (attention.h attn_merge_kernel, mode 2);
+// SLI_ONESHOT_SLICED=0: the separate one-shot residual sum in one workgroup (A/B measurement)
+static bool sliced_oneshot() {
+    static const bool v = [] {
+        const char* e = getenv("SLI_ONESHOT_SLICED");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 // SLI_ATTN_MERGE_LAUNCH=0 keeps the last-arriver merge inside the attention launch (A/B measurement)
 static int defer_batched() {
     static const int v = [] {
@@ -700,8 +709,11 @@ struct StepRecorder {
         a.epoch = m->os_epoch;
         a.st = m->st;
         a.loopback = m->os_loopback;
-        if (max_u64)
+        if (max_u64)  // the argmax keys: 2 * B u64s, one workgroup
             hipLaunchKernelGGL(oneshot_kernel<1>, dim3(1), dim3(1024), 0, m->stream, a);
+        else if (sliced_oneshot())  // the residual sums: sliced over kOsSliceWgs workgroups
+            hipLaunchKernelGGL(oneshot_sliced_kernel, dim3(std::min(kOsSliceWgs, std::max(1, n / 64))), dim3(256), 0,
+                               m->stream, a, m->os_peer_tab, m->os_wg_epoch);
         else
             hipLaunchKernelGGL(oneshot_kernel<0>, dim3(1), dim3(1024), 0, m->stream, a);
         SLI_HIP(hipGetLastError());
@@ -1965,8 +1977,8 @@ int sli_model_comm_handle(sli_model* m, void* out, int32_t n) {
         SLI_HIP(hipMemset(m->os_buf, 0, m->os_bytes));
         SLI_TRY(model_alloc(m, (void**)&m->os_epoch, 16 * sizeof(unsigned)));
         SLI_HIP(hipMemset(m->os_epoch, 0, 16 * sizeof(unsigned)));
-        SLI_TRY(model_alloc(m, (void**)&m->os_wg_epoch, 2 * kOsMaxWg * sizeof(unsigned)));
-        SLI_HIP(hipMemset(m->os_wg_epoch, 0, 2 * kOsMaxWg * sizeof(unsigned)));
+        SLI_TRY(model_alloc(m, (void**)&m->os_wg_epoch, kOsRegions * kOsMaxWg * sizeof(unsigned)));
+        SLI_HIP(hipMemset(m->os_wg_epoch, 0, kOsRegions * kOsMaxWg * sizeof(unsigned)));
         SLI_TRY(model_alloc(m, (void**)&m->os_peer_tab, sizeof(char*) * kOsMaxRanks));
     }
     hipIpcMemHandle_t h;

@@ -25,12 +25,16 @@ namespace sli {
 constexpr int kOsMaxRanks = 8;
 constexpr unsigned kOsSpinLimit = 1u << 24;  // bounded wait (~seconds): gives up with DevState::error bit 4
 constexpr int kOsErrTimeout = 4;
-// Per-workgroup exchange (EpiPush::wg_mode): flags [region 2][par 2][kOsMaxWg][kOsMaxRanks] u32 after the 256-B
-// header of the launch-level flags, then the data blocks of 8 slots x nmax floats: launch-level par 0 / 1, then
-// region 0 (wo) par 0 / 1, region 1 (down) par 0 / 1.
+// Per-workgroup exchanges (EpiPush::wg_mode, oneshot_sliced_kernel): flags [region 3][par 2][kOsMaxWg][kOsMaxRanks]
+// u32 after the 256-B header of the launch-level flags, then the data blocks of 8 slots x nmax floats: launch-level
+// par 0 / 1, then region 0 (wo) par 0 / 1, region 1 (down) par 0 / 1, region 2 (the sliced launch) par 0 / 1.
+// Per-workgroup epochs live in device memory, [region 3][kOsMaxWg].
 constexpr int kOsMaxWg = 512;
-constexpr size_t kOsDataOff = 256 + sizeof(unsigned) * 2 * 2 * kOsMaxWg * kOsMaxRanks;
-inline size_t os_buffer_bytes(int nmax) { return kOsDataOff + sizeof(float) * 6 * (size_t)kOsMaxRanks * nmax; }
+constexpr int kOsRegions = 3;
+constexpr size_t kOsDataOff = 256 + sizeof(unsigned) * kOsRegions * 2 * kOsMaxWg * kOsMaxRanks;
+inline size_t os_buffer_bytes(int nmax) {
+    return kOsDataOff + sizeof(float) * (2 + 2 * kOsRegions) * (size_t)kOsMaxRanks * nmax;
+}
 
 struct OneShotArgs {
     char* peers[kOsMaxRanks];  // every rank's comm buffer, mapped in this process (own one included)
@@ -65,18 +69,24 @@ __device__ __forceinline__ float* os_wg_data(char* buf, int region, int par, int
 // peers: the ranks' buffers, indexed by a runtime rank — the kernel-argument array, or a device-memory table
 // (a runtime index into a struct held in a per-thread copy, as the GEMV epilogues are, would put the whole
 // struct in scratch memory)
+// SLI_OS_FENCE=0: relaxed flag store / poll here too (every comm-buffer access is uncached and drained first,
+// as in EpiPush::finish_wg); 1 (default): system-scope release / acquire.
+#ifndef SLI_OS_FENCE
+#define SLI_OS_FENCE 1
+#endif
 template <int OP>
 __device__ __forceinline__ void os_finish(const OneShotArgs& a, char* const* peers, unsigned e, int* abort_lds) {
+    constexpr int kRel = SLI_OS_FENCE ? __ATOMIC_RELEASE : __ATOMIC_RELAXED;
+    constexpr int kAcq = SLI_OS_FENCE ? __ATOMIC_ACQUIRE : __ATOMIC_RELAXED;
     const int par = (int)(e & 1u);
     const int tid = threadIdx.x, nthr = blockDim.x;
     if (tid < a.nranks)
-        __hip_atomic_store(os_flag(peers[tid], par, a.loopback ? tid : a.rank), e, __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(os_flag(peers[tid], par, a.loopback ? tid : a.rank), e, kRel, __HIP_MEMORY_SCOPE_SYSTEM);
     if (tid == 0) *abort_lds = 0;
     __syncthreads();
     if (tid < a.nranks) {
         unsigned* f = os_flag(peers[a.rank], par, tid);
-        for (unsigned spins = 0; __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != e; ++spins) {
+        for (unsigned spins = 0; __hip_atomic_load(f, kAcq, __HIP_MEMORY_SCOPE_SYSTEM) != e; ++spins) {
             if (spins >= kOsSpinLimit) {
                 __hip_atomic_fetch_or(&a.st->error, kOsErrTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 *abort_lds = 1;
@@ -153,6 +163,67 @@ __global__ void __launch_bounds__(1024) oneshot_kernel(OneShotArgs a) {
     os_finish<OP>(a, a.peers, e, &abort);
 }
 
+// The separate one-shot sum sliced over workgroups (region 2): workgroup w of every rank owns the same slice of the
+// n floats; it pushes its slice of the partial into slot [rank] of every rank, raises flag[2][par][w][rank] on
+// every rank (relaxed: every comm-buffer access is uncached and the pushes have drained), waits (bounded) for the
+// N flags of w in its own buffer and sums its slice of the N slots in rank order into dst. A single summing
+// workgroup moved N x B*D floats each way alone: 33 us per exchange at batch 8 (Llama-3-8B TP 8, loopback).
+// Every workgroup waits for the same workgroup of the peers, so the grid is small (kOsSliceWgs, 256 threads
+// each): ranks sharing one device (tests) still find room on the CUs for each other's workgroups.
+constexpr int kOsSliceWgs = 64;
+__global__ void __launch_bounds__(256) oneshot_sliced_kernel(OneShotArgs a, char* const* peer_tab, unsigned* wg_epoch) {
+    const int w = blockIdx.x, nw = gridDim.x, tid = threadIdx.x;
+    const unsigned e = wg_epoch[2 * kOsMaxWg + w] + 1;  // this workgroup index's previous sliced exchange
+    const int par = (int)(e & 1u);
+    const int n4 = a.n >> 2;  // fp32 sums: n is a multiple of 4 (B * D)
+    const int i0 = (int)(((long long)w * n4) / nw), i1 = (int)(((long long)(w + 1) * n4) / nw);
+    const float4* s4 = reinterpret_cast<const float4*>(a.src);
+    for (int p = 0; p < a.nranks; ++p) {
+        float4* d4 = reinterpret_cast<float4*>(os_wg_data(peer_tab[p], 2, par, a.rank, a.nmax));
+        for (int i = i0 + tid; i < i1; i += blockDim.x) d4[i] = s4[i];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every pushing wave drains before the flags
+    __syncthreads();
+    __shared__ int abort;
+    if (tid < a.nranks)
+        __hip_atomic_store(os_wg_flag(peer_tab[tid], 2, par, w, a.loopback ? tid : a.rank), e, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    if (tid == 0) abort = 0;
+    __syncthreads();
+    if (tid < a.nranks) {
+        const unsigned* f = os_wg_flag(peer_tab[a.rank], 2, par, w, tid);
+        for (unsigned spins = 0; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e; ++spins) {
+            if (spins >= kOsSpinLimit) {
+                __hip_atomic_fetch_or(&a.st->error, kOsErrTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                abort = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __syncthreads();
+    char* mine = peer_tab[a.rank];
+    for (int i = i0 + tid; i < i1; i += blockDim.x) {
+        float4 v[kOsMaxRanks];  // every rank's slot in flight at once, then summed in rank order
+#pragma unroll
+        for (int r = 0; r < kOsMaxRanks; ++r)
+            v[r] = reinterpret_cast<const float4*>(os_wg_data(mine, 2, par, min(r, a.nranks - 1), a.nmax))[i];
+        float4 acc = v[0];
+#pragma unroll
+        for (int r = 1; r < kOsMaxRanks; ++r) {
+            if (r < a.nranks) {
+                acc.x += v[r].x;
+                acc.y += v[r].y;
+                acc.z += v[r].z;
+                acc.w += v[r].w;
+            }
+        }
+        if (abort) acc = float4{__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
+        reinterpret_cast<float4*>(a.dst)[i] = acc;
+    }
+    if (tid == 0) wg_epoch[2 * kOsMaxWg + w] = e;
+}
+
 // The residual all-reduce fused into the row-parallel GEMV that produces the partial (wo, down; batch 1):
 // the epilogue pushes each finished row sum (rank 0: plus the residual) straight into slot [rank] of every
 // rank's comm buffer instead of a local partial; every workgroup drains its pushes and counts its arrival,
@@ -177,7 +248,7 @@ struct EpiPush {
     // fit it together: SLI_DEBUG_GEMV_MAX_BLOCKS in the one-GPU tests).
     int wg_mode = 0;
     int region = 0;              // 0: wo, 1: down (their grids map rows to workgroups differently)
-    unsigned* wg_epoch = nullptr;  // [2][kOsMaxWg]
+    unsigned* wg_epoch = nullptr;  // [kOsRegions][kOsMaxWg]
     unsigned e = 0;
     int pre_u = -1;
     float pre_r[R] = {}, pre_s[R] = {};
