@@ -68,10 +68,10 @@ def parse():
                     help="launches: one graph of fused launches (default, fastest measured); persistent: the whole "
                          "step as one launch with grid barriers (batch 1, TP 1; DESIGN.md §4)")
     ap.add_argument("--tp-allreduce", default="auto", choices=["auto", "rccl", "oneshot", "fused", "fused_wg"],
-                    help="TP all-reduce: auto = the one-shot exchange fused into the wo / down launches (batch 1: "
-                         "per workgroup when every rank has its own GPU, else one summing workgroup; the separate "
-                         "one-shot kernel at batch > 1) if a validation step against RCCL agrees on every rank, "
-                         "else RCCL")
+                    help="TP all-reduce: auto = the one-shot exchange fused into the wo / down launches per "
+                         "workgroup when every rank has its own GPU (else batch 1: one summing workgroup per launch, "
+                         "batch > 1: the sliced one-shot launch) if a validation step against RCCL agrees on every "
+                         "rank, else RCCL")
     ap.add_argument("--prefill-tokens", type=int, default=512,
                     help="after the decode timing: prefill a prompt of this many tokens (0: skip; batch 1 only)")
     ap.add_argument("--prefill-reps", type=int, default=3, help="timed prefill repetitions (after one warm-up)")
@@ -237,11 +237,12 @@ def main():
     allreduce = "none"
     if dist_on:
         allreduce = "rccl"
-        # auto: batch 1 exchanges inside wo / down, per workgroup when every rank has a GPU of its own (ranks
-        # sharing one would starve each other of CUs), else through one summing workgroup per launch
+        # auto: the exchange inside wo / down per workgroup (batch 1: the GEMV; batch > 1: per MFMA group) when
+        # every rank has a GPU of its own (ranks sharing one would starve each other of CUs), else batch 1 through
+        # one summing workgroup per launch, batch > 1 through the sliced one-shot launch
         own_gpu = world <= max(1, torch.cuda.device_count())
         os_mode = (a.tp_allreduce if a.tp_allreduce in ("oneshot", "fused", "fused_wg")
-                   else ("fused_wg" if own_gpu else "fused") if B == 1 else "oneshot")
+                   else "fused_wg" if own_gpu else ("fused" if B == 1 else "oneshot"))
         if os.environ.get("SLI_DEBUG_NOCOMM") and a.tp_allreduce != "rccl":
             # debug (several ranks on one GPU, no RCCL communicator): the one-shot kernels are the only exchange
             from simplellminference_amd import tp

@@ -750,6 +750,7 @@ struct StepRecorder {
     static int prepare(sli_model* m) {
         SLI_TRY((allow<BgEpiQKV<KT>, true>(m)));
         SLI_TRY((allow<BgEpiStore, false>(m)));
+        SLI_TRY((allow<BgEpiPush, false>(m)));
         SLI_TRY((allow<BgEpiSwiGLU, true>(m)));
         SLI_TRY((allow<BgEpiLogits, true>(m)));
         return SLI_OK;
@@ -772,10 +773,35 @@ struct StepRecorder {
                        m->hq, m->hkv, m->hd, m->T};
         return bg(m, m->bg_tiled ? m->layers[l].qkv_t : m->layers[l].qkv, bin(m, m->x, m->norms + (size_t)(2 * l) * m->D, m->D), e, m->bp_qkv);
     }
+    // batched wo / down with the exchange per group (oneshot.h BgEpiPush; region 3: wo, 4: down)
+    static BgEpiPush push_bg(sli_model* m, int region, const BgPlan& p) {
+        BgEpiPush e{};
+        e.resid = m->c.tp_rank == 0 ? m->x : nullptr;
+        for (int r = 0; r < m->c.tp_size; ++r) e.os.peers[r] = m->os_peer[r];
+        e.os.rank = m->c.tp_rank;
+        e.os.nranks = m->c.tp_size;
+        e.os.n = m->B * m->D;
+        e.os.nmax = m->os_nmax;
+        e.os.dst = m->x;
+        e.os.epoch = m->os_epoch;
+        e.os.st = m->st;
+        e.os.loopback = m->os_loopback;
+        e.peer_tab = m->os_peer_tab;
+        e.wg_epoch = m->os_wg_epoch;
+        e.region = region;
+        e.nrows = m->D;
+        e.ld = m->D;
+        e.B = m->B;
+        e.tpw = p.tpw;
+        e.ntiles = p.ntiles;
+        return e;
+    }
     static int b_wo(sli_model* m, int l) {
         const bool tp = m->partial;
+        const void* w = m->bg_tiled ? m->layers[l].wo_t : m->layers[l].wo;
+        if (fused_ar(m)) return bg(m, w, bin(m, m->attn, nullptr, m->hq * m->hd), push_bg(m, 3, m->bp_wo), m->bp_wo);
         BgEpiStore e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, nullptr, 1.0f, m->D, m->D};
-        return bg(m, m->bg_tiled ? m->layers[l].wo_t : m->layers[l].wo, bin(m, m->attn, nullptr, m->hq * m->hd), e, m->bp_wo);
+        return bg(m, w, bin(m, m->attn, nullptr, m->hq * m->hd), e, m->bp_wo);
     }
     static int b_gu(sli_model* m, int l) {
         BgEpiSwiGLU e{m->act, m->Il, m->c.act_mode};
@@ -783,8 +809,10 @@ struct StepRecorder {
     }
     static int b_down(sli_model* m, int l) {
         const bool tp = m->partial;
+        const void* w = m->bg_tiled ? m->layers[l].down_t : m->layers[l].down;
+        if (fused_ar(m)) return bg(m, w, bin(m, m->act, nullptr, m->Il), push_bg(m, 4, m->bp_down), m->bp_down);
         BgEpiStore e{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, nullptr, 1.0f, m->D, m->D};
-        return bg(m, m->bg_tiled ? m->layers[l].down_t : m->layers[l].down, bin(m, m->act, nullptr, m->Il), e, m->bp_down);
+        return bg(m, w, bin(m, m->act, nullptr, m->Il), e, m->bp_down);
     }
     static int b_lm(sli_model* m) {
         BgEpiLogits e{m->logits, m->keys, m->v_n, m->v_n, m->v_lo, m->key_ld};
@@ -1367,7 +1395,7 @@ static int create_model(const sli_model_config* cfg, const void* comm_id, sli_tp
     A((void**)&m->attn_count, sizeof(unsigned) * B * m->hkv);   // per-kv-head arrival counters (kept zero)
     size_t bg_part = 0;
     int bg_groups = 1;
-    const int cus = device_cus();
+    const int cus = gemv_max_blocks();  // device_cus(), or the tests' SLI_DEBUG_GEMV_MAX_BLOCKS cap
     m->key_ld = gemv_max_blocks();  // LM-head argmax keys: one per GEMV workgroup
     if (B > 1) {  // tilings of the batched projections (bgemm.h)
         m->bp_qkv = bg_plan(qkv_rows / 16, D, B, true, cus);
@@ -2026,10 +2054,11 @@ int sli_model_set_allreduce(sli_model* m, int32_t mode) {
     SLI_CHECK(mode == SLI_ALLREDUCE_RCCL || mode == SLI_ALLREDUCE_ONESHOT || mode == SLI_ALLREDUCE_FUSED ||
                   mode == SLI_ALLREDUCE_FUSED_WG,
               SLI_ERR_ARG, "unknown all-reduce mode");
-    SLI_CHECK((mode != SLI_ALLREDUCE_FUSED && mode != SLI_ALLREDUCE_FUSED_WG) || m->B == 1, SLI_ERR_STATE,
-              "the fused all-reduce rides the batch-1 GEMV epilogues (batch > 1: oneshot or rccl)");
-    SLI_CHECK(mode != SLI_ALLREDUCE_FUSED_WG || gemv_max_blocks() <= kOsMaxWg, SLI_ERR_SHAPE,
-              "per-workgroup exchange: more GEMV workgroups than flag slots");
+    SLI_CHECK(mode != SLI_ALLREDUCE_FUSED || m->B == 1, SLI_ERR_STATE,
+              "the launch-level fused all-reduce rides the batch-1 GEMV epilogues (batch > 1: fused_wg, oneshot or rccl)");
+    SLI_CHECK(mode != SLI_ALLREDUCE_FUSED_WG ||
+                  (gemv_max_blocks() <= kOsMaxWg && m->bp_wo.groups <= kOsMaxWg && m->bp_down.groups <= kOsMaxWg),
+              SLI_ERR_SHAPE, "per-workgroup exchange: more workgroups than flag slots");
     SLI_CHECK(mode == SLI_ALLREDUCE_RCCL || m->os_open, SLI_ERR_STATE, "one-shot all-reduce: open the peers first");
     SLI_CHECK(mode == SLI_ALLREDUCE_RCCL || !m->os_dead, SLI_ERR_STATE,
               "one-shot all-reduce: a wait timed out earlier, the ranks' epochs may disagree");

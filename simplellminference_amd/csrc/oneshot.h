@@ -17,6 +17,7 @@
 // identically (one thread of every call), so the captured graph replays it.
 #pragma once
 #include "common.h"
+#include "bgemm.h"
 #include "gemv.h"
 #include "step_state.h"
 
@@ -27,10 +28,11 @@ constexpr unsigned kOsSpinLimit = 1u << 24;  // bounded wait (~seconds): gives u
 constexpr int kOsErrTimeout = 4;
 // Per-workgroup exchanges (EpiPush::wg_mode, oneshot_sliced_kernel): flags [region 3][par 2][kOsMaxWg][kOsMaxRanks]
 // u32 after the 256-B header of the launch-level flags, then the data blocks of 8 slots x nmax floats: launch-level
-// par 0 / 1, then region 0 (wo) par 0 / 1, region 1 (down) par 0 / 1, region 2 (the sliced launch) par 0 / 1.
-// Per-workgroup epochs live in device memory, [region 3][kOsMaxWg].
+// par 0 / 1, then region 0 (batch-1 wo) par 0 / 1, region 1 (batch-1 down), region 2 (the sliced launch), region 3
+// (batched wo, BgEpiPush), region 4 (batched down). Per-workgroup epochs live in device memory,
+// [kOsRegions][kOsMaxWg].
 constexpr int kOsMaxWg = 512;
-constexpr int kOsRegions = 3;
+constexpr int kOsRegions = 5;
 constexpr size_t kOsDataOff = 256 + sizeof(unsigned) * kOsRegions * 2 * kOsMaxWg * kOsMaxRanks;
 inline size_t os_buffer_bytes(int nmax) {
     return kOsDataOff + sizeof(float) * (2 + 2 * kOsRegions) * (size_t)kOsMaxRanks * nmax;
@@ -223,6 +225,78 @@ __global__ void __launch_bounds__(256) oneshot_sliced_kernel(OneShotArgs a, char
     }
     if (tid == 0) wg_epoch[2 * kOsMaxWg + w] = e;
 }
+
+// The batched (bgemm) wo / down with the exchange per group (SLI_ALLREDUCE_FUSED_WG, batch > 1): group g of every
+// rank owns the same tiles, so its rows (x [B][D]: row r of every sequence b) are the same on every rank. The
+// group's final stores go into slot [rank] of every rank (rank 0: plus the residual) instead of xpart; its
+// finishing workgroup drains them, raises flag[region][par][g][rank] on every rank (relaxed: uncached, drained),
+// waits (bounded) for the N flags of g and sums its rows' N slots in rank order into x. Regions 3 (wo) and 4
+// (down); epochs per (region, group).
+struct BgEpiPush {
+    const float* resid;  // rank 0: the residual stream x [B][D]; other ranks nullptr
+    OneShotArgs os;      // dst = x, n = B * D, nmax
+    char* const* peer_tab;
+    unsigned* wg_epoch;  // [kOsRegions][kOsMaxWg]
+    int region;
+    int nrows, ld, B, tpw, ntiles;
+    __device__ int row(int t, int i) const { return min(t * 16 + i, nrows - 1); }
+    __device__ unsigned epoch(int g) const { return wg_epoch[region * kOsMaxWg + g] + 1; }
+    __device__ void one(int row, int b, float v, int par) const {
+        if (row >= nrows) return;
+        const size_t o = (size_t)b * ld + row;
+        const float a = resid ? resid[o] + v : v;  // add_kernel.cpp:5-14, once (rank 0)
+#pragma unroll
+        for (int p = 0; p < kOsMaxRanks; ++p)
+            if (p < os.nranks) os_wg_data(os.peers[p], region, par, os.rank, os.nmax)[o] = a;
+    }
+    // the group index is not passed to store(): the epoch parity comes from the tile's group (t / tpw)
+    __device__ void store(int t, int i, int b, float v0, float v1, unsigned long long*) const {
+        const int par = (int)(epoch(t / tpw) & 1u);
+        one(t * 16 + i, b, v0, par);
+        one(t * 16 + i + 8, b, v1, par);
+    }
+    __device__ void finish(unsigned long long* kl, int g, int) const {
+        const int tid = threadIdx.x;
+        const unsigned e = epoch(g);
+        const int par = (int)(e & 1u);
+        int* abort_lds = reinterpret_cast<int*>(kl + 10);  // bgemm scratch past the keys and the split flag
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every pushing wave drains before the flags
+        __syncthreads();
+        if (tid < os.nranks)
+            __hip_atomic_store(os_wg_flag(peer_tab[tid], region, par, g, os.loopback ? tid : os.rank), e, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        if (tid == 0) *abort_lds = 0;
+        __syncthreads();
+        if (tid < os.nranks) {
+            const unsigned* f = os_wg_flag(peer_tab[os.rank], region, par, g, tid);
+            for (unsigned spins = 0; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e; ++spins) {
+                if (spins >= kOsSpinLimit) {
+                    __hip_atomic_fetch_or(&os.st->error, kOsErrTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    *abort_lds = 1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        __syncthreads();
+        const int t0 = g * tpw, ntg = min(tpw, ntiles - t0);
+        const int nr = min(ntg * 16, nrows - t0 * 16);  // the group's rows (the last tile may be partial)
+        char* mine = peer_tab[os.rank];
+        for (int it = tid; it < nr * B; it += blockDim.x) {
+            const int b = it / nr, row = t0 * 16 + (it - b * nr);
+            const size_t o = (size_t)b * ld + row;
+            float v[kOsMaxRanks];  // every rank's slot in flight at once, then summed in rank order
+#pragma unroll
+            for (int r = 0; r < kOsMaxRanks; ++r) v[r] = os_wg_data(mine, region, par, min(r, os.nranks - 1), os.nmax)[o];
+            float acc = v[0];
+#pragma unroll
+            for (int r = 1; r < kOsMaxRanks; ++r)
+                if (r < os.nranks) acc += v[r];
+            os.dst[o] = *abort_lds ? __builtin_nanf("") : acc;
+        }
+        if (tid == 0) wg_epoch[region * kOsMaxWg + g] = e;
+    }
+};
 
 // The residual all-reduce fused into the row-parallel GEMV that produces the partial (wo, down; batch 1):
 // the epilogue pushes each finished row sum (rank 0: plus the residual) straight into slot [rank] of every

@@ -140,6 +140,10 @@ def _preset(name):
     return preset(base, num_hidden_layers=int(layers)) if layers else preset(base)
 
 
+def _prompts(batch):
+    return ([PROMPT, [5, 6, 7]] + [[9 + b, 3, 11, b] for b in range(2, batch)])[:batch]
+
+
 def _oneshot_rank(rank, world, port, name, batch, q, mode="oneshot", w="f16", prefill=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0",
                       SLI_DEBUG_NOCOMM="1")  # no RCCL communicator: the one-shot kernels are the only exchange
@@ -164,7 +168,7 @@ def _oneshot_rank(rank, world, port, name, batch, q, mode="oneshot", w="f16", pr
         elif batch == 1:
             toks, logits = m.predict(PROMPT, 16, want_logits=True)
         else:
-            toks, logits = m.predict_batch([PROMPT, [5, 6, 7]][:batch], 16, want_logits=True)
+            toks, logits = m.predict_batch(_prompts(batch), 16, want_logits=True)
         err = m.state()["error"]
         parts = [torch.zeros(logits.shape, dtype=torch.float32) for _ in range(world)]
         dist.all_gather(parts, torch.from_numpy(np.ascontiguousarray(logits)))
@@ -180,20 +184,23 @@ def _oneshot_rank(rank, world, port, name, batch, q, mode="oneshot", w="f16", pr
 @pytest.mark.parametrize("name,batch,mode", [("tiny", 1, "oneshot"), ("tiny-gqa", 1, "oneshot"), ("tiny-gqa", 2, "oneshot"),
                                              ("tiny", 1, "fused"), ("tiny-gqa", 1, "fused"), ("tiny-h8", 1, "fused"),
                                              ("tiny", 1, "fused_wg"), ("tiny-gqa", 1, "fused_wg"),
-                                             ("tiny-h8", 1, "fused_wg")])
+                                             ("tiny-h8", 1, "fused_wg"), ("tiny-gqa", 2, "fused_wg"),
+                                             ("llama3-8b:2", 8, "fused_wg"), ("llama3-8b:2", 8, "oneshot")])
 def test_oneshot_allreduce_two_processes(gpu, name, batch, mode):
     """The one-shot all-reduce (oneshot.h) between two rank PROCESSES through IPC-mapped uncached buffers
     (both on device 0 here; on the 8-GPU node each on its own GPU, over xGMI): greedy tokens identical to
     the TP = 1 engine, logits within 1e-3, no device error (the bounded waits never gave up). mode "fused":
     the exchange runs inside the wo / down GEMV launches (EpiPush: rows pushed from the epilogue, the
     launch's last workgroup waits and sums); "fused_wg": per workgroup (each waits for the same workgroup of
-    the peer and sums its own rows; the grids capped so both ranks' launches fit the one GPU together)."""
-    from simplellminference_amd.model import LlamaModel, preset
-    ref = LlamaModel(config=preset(name), w_dtype="f16", kv_dtype="f16", seed=0, batch=batch).init()
+    the peer and sums its own rows; the grids capped so both ranks' launches fit the one GPU together), at batch
+    > 1 inside the MFMA wo / down (BgEpiPush, per group). "llama3-8b:2": the C4 shard shapes at TP 2 (2 layers,
+    batch 8): the per-group exchange and the sliced one-shot launch."""
+    from simplellminference_amd.model import LlamaModel
+    ref = LlamaModel(config=_preset(name), w_dtype="f16", kv_dtype="f16", seed=0, batch=batch).init()
     if batch == 1:
         rtoks, rlogits = ref.predict(PROMPT, 16, want_logits=True)
     else:
-        rtoks, rlogits = ref.predict_batch([PROMPT, [5, 6, 7]][:batch], 16, want_logits=True)
+        rtoks, rlogits = ref.predict_batch(_prompts(batch), 16, want_logits=True)
     ref.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
