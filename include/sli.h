@@ -155,10 +155,11 @@ int sli_tp_vocab(const sli_model_config* cfg, int32_t* vocab_lo, int32_t* vocab_
  * SLI_ALLREDUCE_FUSED (batch 1): the same exchange inside the wo / down GEMV launches — their epilogues
  * push the finished rows into the peers' slots and the launch's last workgroup waits and sums (no
  * separate all-reduce launch).
- * SLI_ALLREDUCE_FUSED_WG (batch 1, ranks on distinct devices): the fused exchange per workgroup — workgroup w
- * of every rank owns the same rows, waits for the same workgroup of the peers and sums its own rows (no
- * launch-wide arrival, no single summing workgroup). Every workgroup waits, so ranks sharing one device
- * would starve each other of CUs unless their grids fit together (SLI_DEBUG_GEMV_MAX_BLOCKS). */
+ * SLI_ALLREDUCE_FUSED_WG (ranks on distinct devices, any batch): the fused exchange per workgroup — workgroup w
+ * (batch > 1: MFMA group g) of every rank owns the same rows, waits for the same workgroup of the peers and
+ * sums its own rows (no launch-wide arrival, no single summing workgroup). Every workgroup waits, so ranks
+ * sharing one device would starve each other of CUs unless their grids fit together
+ * (SLI_DEBUG_GEMV_MAX_BLOCKS). The separate ONESHOT sum is sliced over workgroups the same way. */
 enum { SLI_ALLREDUCE_RCCL = 0, SLI_ALLREDUCE_ONESHOT = 1, SLI_ALLREDUCE_FUSED = 2, SLI_ALLREDUCE_FUSED_WG = 3 };
 int sli_model_comm_handle_bytes(void);
 int sli_model_comm_handle(sli_model* m, void* out, int32_t n);
