@@ -180,13 +180,15 @@ static int mha_launch_hd(const float* q, const KT* kc, const KT* vc, float* out,
     // the same K/V rows. Deferred merges only (partials are indexed by q head; the counters by kv head).
     // Measured (profiles/r4_gqa_split_ab.txt): Llama-3-8B batch 1 ctx 4096 (8 kv heads x 16 splits = 128
     // workgroups on 256 CUs) attention 10.7 -> 8.1 us with 2 (287 -> 292 tok/s), 9.2 with 4; C4 (batch 8,
-    // 1024 workgroups) 34.5 -> 41 us with 2, 55 with 4. Default: 2 where the unsplit grid fills at most half the
-    // chip and the consumer merges (batch 1), else off. SLI_ATTN_GQA_SPLIT=1|2|4 forces it.
+    // 1024 workgroups) 34.5 -> 41 us with 2, 55 with 4; C4's TP-8 shard (batch 8 x 1 kv head x 16 splits = 128
+    // workgroups, merge launch) 14.5 -> 11.9 us with 2, 12.6 with 4 (profiles/r4_c4_tp_families.txt). Default: 2
+    // where the unsplit grid fills at most half the chip and the merge is deferred, else off.
+    // SLI_ATTN_GQA_SPLIT=1|2|4 forces it.
     static const int gqa_env = [] {
         const char* e = getenv("SLI_ATTN_GQA_SPLIT");
         return e && (e[0] == '1' || e[0] == '2' || e[0] == '4') ? e[0] - '0' : 0;
     }();
-    const int gqa_split = gqa_env ? gqa_env : (defer_merge == 1 && 2 * Hkv * wg_splits <= device_cus() ? 2 : 1);
+    const int gqa_split = gqa_env ? gqa_env : (defer_merge != 0 && 2 * Hkv * wg_splits <= device_cus() ? 2 : 1);
     if (gqa_split > 1 && g == 4 && defer_merge && cache_heads == 0) {
         g /= gqa_split;
         a.kv_group = gqa_split;
