@@ -324,8 +324,20 @@ __device__ __forceinline__ int attn_live_splits(const AttnArgs<KT>& a, int kvh) 
 
 // grid: n_kv_heads * wg_splits workgroups of 64 * WAVES threads
 template <typename KT, int HD, int G, int WAVES = attn_waves(G), bool LATE_V = attn_late_v(G)>
+// Stagger (C4: 1024 workgroups, two per CU, two residency rounds): each round is a K burst, the scores, a V burst
+// and the merge, with HBM idle between the bursts. Workgroups 256..511 (the second of each CU in the first
+// round, under the dispatcher's order) start SLI_ATTN_STAGGER x 0.85 us later, so their K burst overlaps the
+// first workgroup's scores; later rounds stagger by themselves. Measured at C4 (profiles/r4_attn_stagger_ab.txt):
+// 0 / 1.7 / 3.4 / 6.8 / 13.6 us = attention 34.95 / 34.24 / 34.18 / 35.09 / 44.56 us. 0: off.
+#ifndef SLI_ATTN_STAGGER
+#define SLI_ATTN_STAGGER 4
+#endif
 __global__ void __launch_bounds__(64 * WAVES) attn_partial_kernel(AttnArgs<KT> a) {
     if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 4] = __builtin_amdgcn_s_memrealtime();
+#if SLI_ATTN_STAGGER
+    if (G == 4 && gridDim.x >= 1024 && blockIdx.x >= 256 && blockIdx.x < 512)
+        for (int i = 0; i < SLI_ATTN_STAGGER; ++i) __builtin_amdgcn_s_sleep(32);
+#endif
     const int kvh = blockIdx.x / a.max_splits;  // max_splits counts workgroup splits here
     if (attn_publish<KT, HD, G, WAVES, LATE_V>(a, kvh, blockIdx.x - kvh * a.max_splits)) {
         attn_merge<HD, G>(a.part, a.out, kvh, a.max_splits, attn_live_splits<KT, HD, G>(a, kvh), 0, 64 * WAVES);
