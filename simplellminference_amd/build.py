@@ -51,7 +51,9 @@ def _compile(src: str, force: bool, build_dir: str = BUILD, defines: tuple = ())
     if not force and os.path.exists(obj) and os.path.getmtime(obj) >= newest_dep:
         return obj
     lang = ["-x", "hip"] if src.endswith(".cpp") else []
-    cmd = ["hipcc", *lang, *CXXFLAGS, *[f"-D{d}" for d in defines], "-c", src, "-o", obj]
+    # SLI_EXTRA_CXXFLAGS: extra compiler flags for an A/B variant build (tools/ab_variants.sh), e.g. code alignment
+    extra = os.environ.get("SLI_EXTRA_CXXFLAGS", "").split() if build_dir != BUILD else []
+    cmd = ["hipcc", *lang, *CXXFLAGS, *extra, *[f"-D{d}" for d in defines], "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

@@ -159,6 +159,11 @@ __device__ __forceinline__ void bg_split8(const float* y, u32x4& hi, u32x4& lo) 
 //   store(t, i, b, v0, v1, kl)  final sums of tile rows i (< 8) and i + 8 for sequence b; kl = the
 //                               workgroup's per-sequence argmax keys in LDS
 //   finish(kl, group, B)        once per workgroup that ran stores, after all of them
+//   pre_a(t0, ntg, B), pre_b()  the epilogue's own inputs for this thread's first item (it = tid: tile t0 +
+//                               (it >> 6), row pair (it >> 3) & 7, sequence it & 7), issued before the
+//                               activation loads (pre_a) and right after the first weight steps (pre_b, for
+//                               loads that depend on pre_a's), so they land during the stream instead of
+//                               costing a round trip after it
 template <class Epi, bool NORM, int kBgU = 4>
 __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restrict__ W, BgIn in, Epi epi_in) {
     Epi epi = epi_in;
@@ -188,6 +193,7 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
 
     if (tid < kBgMaxBatch) keys[tid] = 0ull;
     const unsigned long long t_entry = in.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+    epi.pre_a(t0, ntg, B);
 
     // ---- 1. activation staging loads, issued first (s_waitcnt vmcnt counts in issue order). Thread t
     // stages sequence b = t & 7 at the 8-k groups (t >> 3) + 128 n: the 8 lanes of a group write 8
@@ -251,6 +257,7 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
     load_step(0, wa);
     load_step(1, wb);
     __builtin_amdgcn_sched_barrier(0);
+    epi.pre_b();
 
     // ---- 3./4. this wave's blocks into LDS as B fragments (hi: column b, lo: 8 + b), visible to the
     // wave's own later reads after lgkmcnt(0); NORM: x * w staged, this wave's sum of x^2 to red[wave][b]
@@ -410,6 +417,9 @@ struct BgEpiStore {
     int nrows;
     int ld;  // per-sequence stride of y / resid
     __device__ int row(int t, int i) const { return min(t * 16 + i, nrows - 1); }
+    // (prefetching the residuals measured slower: C4 wo 8.89 -> 9.21 us, profiles/r4_bg_epi_prefetch_ab.txt)
+    __device__ void pre_a(int, int, int) {}
+    __device__ void pre_b() {}
     __device__ void one(int row, int b, float v) const {
         if (row >= nrows) return;
         float a = rscale ? v * rscale[row] : v;
@@ -439,6 +449,27 @@ struct BgEpiQKV {
     int hq, hkv, hd, T;
     int kv_seq = 1;  // 1: sequence b owns cache heads [b*hkv, (b+1)*hkv); 0: one cache shared by every lane
                      // (prefill lanes of one sequence at consecutive positions)
+    int prefetch = 1;  // 0: no epilogue prefetch (A/B: SLI_BG_EPI_PREFETCH=0)
+    int p_t = -1, p_i = 0, p_b = 0, p_pos = 0;  // the prefetched item: its position, then its RoPE row
+    float p_sin = 0.0f, p_cos = 0.0f;
+    __device__ void pre_a(int t0, int ntg, int B) {
+        const int it = threadIdx.x;
+        if (!prefetch || it >= ntg * 64 || (it & 7) >= B) return;
+        p_t = t0 + (it >> 6);
+        p_i = (it >> 3) & 7;
+        p_b = it & 7;
+        p_pos = pos_dev[(size_t)p_b * pos_stride];
+    }
+    __device__ void pre_b() {
+        if (p_t < 0) return;
+        const int half = hd >> 1;
+        const int u = p_t * 8 + p_i;
+        const int uh = u / half, d = u - uh * half;
+        if (uh < hq + hkv) {
+            p_sin = sin_t[p_pos * half + d];
+            p_cos = cos_t[p_pos * half + d];
+        }
+    }
     __device__ int row(int t, int i) const {
         const int half = hd >> 1;
         const int u = t * 8 + (i & 7);
@@ -449,9 +480,10 @@ struct BgEpiQKV {
         const int half = hd >> 1;
         const int u = t * 8 + i;
         const int uh = u / half, d = u - uh * half;
-        const int pos = pos_dev[(size_t)b * pos_stride];
+        const bool pre = t == p_t && i == p_i && b == p_b;
+        const int pos = pre ? p_pos : pos_dev[(size_t)b * pos_stride];
         if (uh < hq + hkv) {  // rope_kernel.cpp:30-38
-            const float fci = sin_t[pos * half + d], fcr = cos_t[pos * half + d];
+            const float fci = pre ? p_sin : sin_t[pos * half + d], fcr = pre ? p_cos : cos_t[pos * half + d];
             const float r0 = a0 * fcr - a1 * fci;
             const float r1 = a1 * fcr + a0 * fci;
             if (uh < hq) {
@@ -479,6 +511,8 @@ struct BgEpiSwiGLU {
     int inter;
     int silu;
     __device__ int row(int t, int i) const { return t * 8 + (i & 7) + (i >= 8 ? inter : 0); }
+    __device__ void pre_a(int, int, int) {}
+    __device__ void pre_b() {}
     __device__ void store(int t, int i, int b, float g, float up, unsigned long long*) const {
         float sg = 1.0f / (1.0f + expf(-g));  // swiglu_kernel.cpp:12
         if (silu) sg = g * sg;
@@ -494,6 +528,8 @@ struct BgEpiLogits {
     unsigned long long* keys_out;  // [B][key_ld]
     int nrows, ld, vocab_off, key_ld;
     __device__ int row(int t, int i) const { return min(t * 16 + i, nrows - 1); }
+    __device__ void pre_a(int, int, int) {}
+    __device__ void pre_b() {}
     __device__ void one(int row, int b, float v, unsigned long long* kl) const {
         if (row >= nrows) return;
         logits[(size_t)b * ld + row] = v;

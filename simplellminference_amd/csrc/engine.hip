@@ -524,6 +524,15 @@ __global__ void group_finalize_kernel(GroupKeyArgs a) {
 
 
 // batched decode: the attention's split merge as its own launch (attention.h attn_merge_kernel, mode 2);
+// SLI_BG_EPI_PREFETCH=0: the batched q/k/v epilogue loads its position and RoPE row after the stream (A/B)
+static bool bg_epi_prefetch() {
+    static const bool v = [] {
+        const char* e = getenv("SLI_BG_EPI_PREFETCH");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 // SLI_ONESHOT_SLICED=0: the separate one-shot residual sum in one workgroup (A/B measurement)
 static bool sliced_oneshot() {
     static const bool v = [] {
@@ -771,6 +780,7 @@ struct StepRecorder {
         const size_t lay = (size_t)l * m->B * m->hkv * m->T * m->hd;
         BgEpiQKV<KT> e{m->q, (KT*)m->kc + lay, (KT*)m->vc + lay, &m->st->pos, kPosStride, m->sin_t, m->cos_t,
                        m->hq, m->hkv, m->hd, m->T};
+        e.prefetch = bg_epi_prefetch() ? 1 : 0;
         return bg(m, m->bg_tiled ? m->layers[l].qkv_t : m->layers[l].qkv, bin(m, m->x, m->norms + (size_t)(2 * l) * m->D, m->D), e, m->bp_qkv);
     }
     // batched wo / down with the exchange per group (oneshot.h BgEpiPush; region 3: wo, 4: down)

@@ -240,6 +240,8 @@ struct BgEpiPush {
     int region;
     int nrows, ld, B, tpw, ntiles;
     __device__ int row(int t, int i) const { return min(t * 16 + i, nrows - 1); }
+    __device__ void pre_a(int, int, int) {}
+    __device__ void pre_b() {}
     __device__ unsigned epoch(int g) const { return wg_epoch[region * kOsMaxWg + g] + 1; }
     __device__ void one(int row, int b, float v, int par) const {
         if (row >= nrows) return;
