@@ -220,6 +220,10 @@ def main():
         cid = box[0]
     cfg = preset(a.preset, max_length=a.ctx)
     B = a.batch
+    if dist_on and world <= max(1, torch.cuda.device_count()):
+        # each rank has a GPU of its own: q/k/v + attention as one launch on the shards where it fits
+        # (csrc/qkv_attn.h; its attention workgroups wait inside the launch, so ranks sharing a GPU keep two launches)
+        os.environ.setdefault("SLI_QKV_ATTN", "1")
     model = LlamaModel(config=cfg, w_dtype=a.w_dtype, kv_dtype="f16", tp_rank=rank, tp_size=world, comm_id=cid,
                        device=local, seed=1, batch=B).init()
     exec_mode = a.exec
@@ -360,6 +364,7 @@ def main():
                    "step_frac_of_hbm_peak": round((wbytes + kvbytes) / (ms * 1e-3) / (HBM_PEAK_GBS * 1e9), 4)},
         "exec": exec_mode,
         "tp_allreduce": allreduce,
+        "qkv_attn_fused": model.fused_qkv_attn(),
         "roofline": {"bound": "hbm", "kernel": f"{dom}: {FAMILY_KERNELS[B > 1][dom]}",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_source,

@@ -205,6 +205,13 @@ int sli_model_prefill(sli_model* m, const int32_t* ids, int32_t n);
 /* Which path sli_model_prefill takes for this model: 1 = chunked MFMA GEMMs (prefill.h), 0 = the decode step,
  * teacher-forced (fp32 weights, batch > 1, unsupported shapes, or a TP rank without an RCCL communicator). */
 int sli_model_prefill_path(const sli_model* m);
+/* 1: the batch-1 decode step runs each layer's q/k/v projection and attention as ONE launch (qkv_attn.h: the
+ * attention's K/V rows below the position stream while the projection runs; q and this step's K/V row are
+ * handed over inside the launch), 0: two launches (model.cpp:70-84's matmul / rope / mha sequence either way).
+ * Taken where the shape qualifies (heads per kv head 1 or 2, head_dim 64 / 128, fp16 K/V cache, fp16 / int8
+ * weights, an attention grid of at most a quarter of the CUs) and SLI_QKV_ATTN allows it
+ * (1: always; 0: never; unset: single-rank models). */
+int sli_model_fused_qkv_attn(sli_model* m);
 /* sli_model_predict with the prompt prefilled: tokens_out[t] as sli_model_predict; logits_out rows for
  * positions < n_prompt - 1 (not computed by the prefill) are NaN. */
 int sli_model_predict_prefill(sli_model* m, const int32_t* prompt, int32_t n_prompt, int32_t max_length,

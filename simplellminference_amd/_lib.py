@@ -90,6 +90,7 @@ _SIGS = {
     "sli_model_prefill": (c_int, [c_vp, c_vp, c_i32]),
     "sli_model_predict_prefill": (c_int, [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp]),
     "sli_model_prefill_path": (c_int, [c_vp]),
+    "sli_model_fused_qkv_attn": (c_int, [c_vp]),
     "sli_model_get_history": (c_int, [c_vp, c_i32, c_i32, c_vp]),
     "sli_model_set_exec": (c_int, [c_vp, c_i32]),
     "sli_model_get_exec": (c_int, [c_vp, P_i32]),

@@ -42,7 +42,52 @@ struct AttnArgs {
     int defer_merge = 0;    // != 0: only write the workgroup partials (plain stores); the splits are merged
                             // after the launch: 1 by the consumer (the wo GEMV's input staging, gemv.h
                             // XStageMerge), 2 by attn_merge_kernel (mha_launch launches it)
+    // HAND (the fused q/k/v + attention launch, qkv_attn.h): q and this step's K/V rows are produced by the q/k/v
+    // workgroups of the same launch, stored write-through (sc1) and counted per kv head
+    const float* hand_kv = nullptr;  // [2][n_kv_heads][hd]: this step's k rows, then its v rows (cache-rounded)
+    unsigned* hand_count = nullptr;  // attn_hand_bytes: q/k/v units landed per kv head (kAttnHandSub counters, one
+                                     // per 128-byte line), then live workgroups done per kv head (the last resets)
+    unsigned hand_expect = 0;        // units per kv head: (G + 2) * hd / 2
+    int* hand_err = nullptr;         // DevState::error: a bounded wait that gave up sets kAttnErrHand
 };
+
+constexpr int kAttnErrHand = 8;               // DevState::error bit (persist.h 2, oneshot.h 4)
+constexpr unsigned kAttnHandSpin = 1u << 22;  // bounded wait (~seconds)
+// A kv head's arrivals are spread over kAttnHandSub counters on separate 128-byte lines (producer workgroup b
+// adds to counter b % kAttnHandSub): same-line device-scope atomics serialise (measured: one add per q/k/v unit on
+// one line cost 23 / 45 us per TP-8 / TP-4 launch).
+constexpr int kAttnHandSub = 16;
+constexpr int kAttnHandLine = 32;  // unsigned per 128-byte line
+__host__ __device__ constexpr size_t attn_hand_words(int n_kv_heads) {
+    return (size_t)n_kv_heads * (kAttnHandSub + 1) * kAttnHandLine;
+}
+__host__ __device__ __forceinline__ unsigned* attn_hand_sub(unsigned* c, int kvh, int sub) {
+    return c + ((size_t)kvh * kAttnHandSub + sub) * kAttnHandLine;
+}
+__host__ __device__ __forceinline__ unsigned* attn_hand_done(unsigned* c, int n_kv_heads, int kvh) {
+    return c + ((size_t)n_kv_heads * kAttnHandSub + kvh) * kAttnHandLine;
+}
+
+// HAND: a wave's wait for its kv head's q / k / v units: lanes 0..kAttnHandSub-1 read one counter each, summed
+// across the wave (the first read also waits for the K/V rows issued ahead of it, which the wave needs next anyway).
+template <typename KT>
+__device__ __forceinline__ void attn_hand_wait(const AttnArgs<KT>& a, int kvh) {
+    const int lane = threadIdx.x & 63;
+    unsigned* c = attn_hand_sub(a.hand_count, kvh, min(lane, kAttnHandSub - 1));
+    for (unsigned spins = 0;; ++spins) {
+        const unsigned v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((unsigned)wave_sum(lane < kAttnHandSub ? (float)v : 0.0f) >= a.hand_expect) break;  // exact below 2^24
+        if (spins >= kAttnHandSpin) {
+            __hip_atomic_fetch_or(a.hand_err, kAttnErrHand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+// HAND: one sc1 element of a handed-off vector
+__device__ __forceinline__ float attn_hand_ld(const float* p) {
+    return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // Position of the sequence that owns (batched) kv head kvh.
 template <typename KT>
@@ -94,13 +139,14 @@ __host__ __device__ constexpr bool attn_late_v(int g) { return g == 1 ? SLI_ATTN
 // The split work of workgroup (kvh, wgs): partial state published write-through, arrival counted.
 // Returns true in the head's last-arriving workgroup (which must then merge the head: attn_merge).
 // Every return is uniform over the workgroup.
-template <typename KT, int HD, int G, int WAVES = attn_waves(G), bool LATE_V = attn_late_v(G)>
+template <typename KT, int HD, int G, int WAVES = attn_waves(G), bool LATE_V = attn_late_v(G), bool HAND = false>
 __device__ __forceinline__ bool attn_publish(const AttnArgs<KT>& a, int kvh, int wgs) {
     using Geo = AttnGeom<KT, HD>;
     constexpr int kAttnNit = kAttnSlots / WAVES;
     constexpr int EPV = Geo::EPV, LPR = Geo::LPR, RPI = Geo::RPI, PPW = kAttnNit * RPI;
     __shared__ float sh[WAVES][G][HD + 2];
     __shared__ int last;
+    __shared__ float hs[HAND ? (G + 2) * HD : 1];  // HAND: q (G heads), then this step's k and v rows
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int pos = attn_pos(a, kvh);
@@ -119,7 +165,7 @@ __device__ __forceinline__ bool attn_publish(const AttnArgs<KT>& a, int kvh, int
 #pragma unroll
         for (int e = 0; e < EPV; ++e) ov[g][e] = 0.0f;
     }
-    if (live_wave) {
+    if (HAND || live_wave) {  // HAND: every wave (the workgroup barrier below); a dead wave's state is reset after
         const int ch = a.cache_heads > 0 ? kvh % a.cache_heads : kvh / a.kv_group;
         const KT* kb = a.k + (long long)ch * a.head_stride + li * EPV;
         const KT* vb = a.v + (long long)ch * a.head_stride + li * EPV;
@@ -139,11 +185,49 @@ __device__ __forceinline__ bool attn_publish(const AttnArgs<KT>& a, int kvh, int
         // LATE_V: V is loaded once the scores are done, so K and V never occupy registers together
         // (GQA-4/8 carry G query heads per lane: fewer registers = more resident workgroups)
         if constexpr (!LATE_V) load_v();
+        // HAND: the rows below pos (earlier launches) are in flight. Wave 0 waits for the kv head's q / k / v units
+        // and stages q and this step's K/V rows (sc1, one batch) into LDS for the workgroup; the row at pos then
+        // replaces the (stale) cache row the clamped loads fetched. (One reader per workgroup: sc1 reads of the same
+        // lines by every wave, and every wave polling, measured 16.6 -> 23 us per TP-8 launch.)
+        auto hand_row = [&](u32x4(&r)[kAttnNit], const float* f) {
+#pragma unroll
+            for (int it = 0; it < kAttnNit; ++it) {
+                if (min(t0 + it * RPI + sub, t_end - 1) == pos) {
+                    float x[EPV];
+#pragma unroll
+                    for (int e = 0; e < EPV; ++e) x[e] = f[li * EPV + e];
+                    r[it] = Vec16<KT>::pack(x);
+                }
+            }
+        };
+        if constexpr (HAND) {
+            if (wave == 0) {
+                attn_hand_wait(a, kvh);
+                constexpr int NQ = G * HD, NJ = (G + 2) * HD / 64;
+                float x[NJ];
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    const int i = j * 64 + lane;
+                    const float* src = i < NQ        ? a.q + (size_t)kvh * NQ + i
+                                       : i < NQ + HD ? a.hand_kv + (size_t)kvh * HD + (i - NQ)
+                                                     : a.hand_kv + ((size_t)a.n_kv_heads + kvh) * HD + (i - NQ - HD);
+                    x[j] = attn_hand_ld(src);
+                }
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) hs[j * 64 + lane] = x[j];
+            }
+            __syncthreads();
+        }
         float qv[G][EPV];
 #pragma unroll
         for (int g = 0; g < G; ++g)
 #pragma unroll
-            for (int e = 0; e < EPV; ++e) qv[g][e] = a.q[(size_t)(kvh * G + g) * HD + li * EPV + e];
+            for (int e = 0; e < EPV; ++e)
+                qv[g][e] = HAND ? hs[g * HD + li * EPV + e] : a.q[(size_t)(kvh * G + g) * HD + li * EPV + e];
+        if constexpr (HAND) {
+            hand_row(kr, hs + G * HD);
+            if constexpr (!LATE_V) hand_row(vr, hs + (G + 1) * HD);
+        }
         float s[kAttnNit][G];
 #pragma unroll
         for (int it = 0; it < kAttnNit; ++it) {
@@ -160,7 +244,10 @@ __device__ __forceinline__ bool attn_publish(const AttnArgs<KT>& a, int kvh, int
                 m[g] = fmaxf(m[g], s[it][g]);
             }
         }
-        if constexpr (LATE_V) load_v();
+        if constexpr (LATE_V) {
+            load_v();
+            if constexpr (HAND) hand_row(vr, hs + (G + 1) * HD);
+        }
 #pragma unroll
         for (int g = 0; g < G; ++g)
             m[g] = stride_max<LPR>(m[g]);
@@ -183,6 +270,15 @@ __device__ __forceinline__ bool attn_publish(const AttnArgs<KT>& a, int kvh, int
 #pragma unroll
             for (int e = 0; e < EPV; ++e) ov[g][e] = stride_sum<LPR>(ov[g][e]);
         }
+        if (HAND && !live_wave) {  // (its rows were all masked: the empty state, as a dead wave's)
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                m[g] = -INFINITY;
+                l[g] = 0.0f;
+#pragma unroll
+                for (int e = 0; e < EPV; ++e) ov[g][e] = 0.0f;
+            }
+        }
     }
     if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 4 + 1] = __builtin_amdgcn_s_memrealtime();
     if (sub == 0) {
@@ -197,6 +293,20 @@ __device__ __forceinline__ bool attn_publish(const AttnArgs<KT>& a, int kvh, int
         }
     }
     __syncthreads();
+    if constexpr (HAND) {  // every wave of the workgroup is past its wait: the head's last live workgroup resets
+        if (threadIdx.x < 64) {
+            const int ns = min(pos / (WAVES * PPW) + 1, a.max_splits);
+            unsigned* done = attn_hand_done(a.hand_count, a.n_kv_heads, kvh);
+            unsigned prev = 0;
+            if (threadIdx.x == 0) prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__builtin_amdgcn_readfirstlane(prev) == (unsigned)(ns - 1)) {
+                if (threadIdx.x < kAttnHandSub)
+                    __hip_atomic_store(attn_hand_sub(a.hand_count, kvh, threadIdx.x), 0u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                if (threadIdx.x == 0) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
     if (a.defer_merge) {  // partials for the next launch (the kernel boundary publishes them): plain stores
         for (int i = threadIdx.x; i < G * HD; i += 64 * WAVES) {
             const int g = i / HD, d = i - g * HD;

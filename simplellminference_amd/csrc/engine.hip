@@ -32,6 +32,7 @@
 #include "ops_internal.h"
 #include "persist.h"
 #include "prefill.h"
+#include "qkv_attn.h"
 #include "rope_table.h"
 #include "step_state.h"
 
@@ -78,6 +79,8 @@ struct sli_model {
     float *x = nullptr, *xpart = nullptr, *q = nullptr, *attn = nullptr, *act = nullptr, *logits = nullptr;
     float* part = nullptr;
     unsigned* attn_count = nullptr;
+    float* qa_kv = nullptr;       // batch 1: the fused q/k/v + attention launch's hand-off rows [2][hkv][hd] (qkv_attn.h)
+    unsigned* qa_count = nullptr; // its per-kv-head counters (attention.h attn_hand_words; zero between launches)
     int wo_merge = 1;           // batch 1: 1 = the wo GEMV merges the attention's splits while staging its input,
                                 // 0 = the attention's last-arriving workgroup merges them (wo_merges)
     int wo_ks = 1;              // batch-1 TP-1 wo split over its columns (wo_ksplit): partials [wo_ks][D]
@@ -542,6 +545,19 @@ static bool sliced_oneshot() {
     return v;
 }
 
+// The fused q/k/v + attention launch (qkv_attn.h). SLI_QKV_ATTN=1: wherever the shape qualifies; 0: never;
+// unset: single-rank models only (a rank process that may share its GPU with others keeps the two launches
+// unless the launcher knows each rank has a device of its own: bench.py sets 1 then). In-process groups never
+// (their ranks' launches share one device).
+static bool qkv_attn_on(const sli_model* m) {
+    static const int env = [] {
+        const char* e = getenv("SLI_QKV_ATTN");
+        return e ? (e[0] == '1' ? 1 : 0) : -1;
+    }();
+    if (m->group || env == 0) return false;
+    return env == 1 || !m->partial;
+}
+
 // SLI_ATTN_MERGE_LAUNCH=0 keeps the last-arriver merge inside the attention launch (A/B measurement)
 static int defer_batched() {
     static const int v = [] {
@@ -561,6 +577,35 @@ struct StepRecorder {
         KT* vc = (KT*)m->vc + (size_t)l * m->hkv * m->T * m->hd;
         EpiQKV<KT> e{m->q, kc, vc, w.qkv_s, &m->st->pos, m->sin_t, m->cos_t, m->hq, m->hkv, m->hd, m->T};
         SLI_HIP((launch_gemv_u<WT, 2, 4, NT>((const WT*)w.qkv, in, e, (m->hq + 2 * m->hkv) * (m->hd / 2), m->stream)));
+        return SLI_OK;
+    }
+    // q/k/v + attention as one launch (qkv_attn.h) where the shape qualifies; *done = false: run the two launches
+    static int gemv_qkv_attn(sli_model* m, int l, bool* done, bool dry = false) {
+        *done = false;
+        if constexpr (std::is_same<KT, __half>::value && !std::is_same<WT, float>::value) {
+            if (!m->qa_count || !qkv_attn_on(m)) return SLI_OK;
+            const LayerW& w = m->layers[l];
+            GemvIn in{m->x, m->norms + (size_t)(2 * l) * m->D, m->c.eps, m->D};
+            const size_t lay = (size_t)l * m->hkv * m->T * m->hd;
+            KT* kc = (KT*)m->kc + lay;
+            KT* vc = (KT*)m->vc + lay;
+            const int g = m->hq / m->hkv;
+            EpiQKVHand<KT> e{{m->q, kc, vc, w.qkv_s, &m->st->pos, m->sin_t, m->cos_t, m->hq, m->hkv, m->hd, m->T},
+                             m->qa_kv, m->qa_count, g};
+            const int ppwg = attn_wg_positions(m->c.kv_dtype, m->hd);
+            AttnArgs<KT> a{m->q, kc, vc, m->hd, (long long)m->T * m->hd, m->part, m->attn, m->attn_count, &m->st->pos, 0,
+                           m->hkv, (m->T + ppwg - 1) / ppwg, 1.0f / sqrtf((float)m->hd), m->hkv, 0};
+            a.defer_merge = m->wo_merge;
+            a.hand_kv = m->qa_kv;
+            a.hand_count = m->qa_count;
+            a.hand_expect = (unsigned)((g + 2) * (m->hd / 2));
+            a.hand_err = &m->st->error;
+            const hipError_t r = launch_qkv_attn<WT, KT>((const WT*)w.qkv, in, e, a, (m->hq + 2 * m->hkv) * (m->hd / 2),
+                                                         m->hd, m->stream, dry);
+            if (r == hipErrorNotSupported) return SLI_OK;
+            SLI_HIP(r);
+            *done = true;
+        }
         return SLI_OK;
     }
     // wo + residual; its input is merged from the attention's split partials while it is staged
@@ -852,6 +897,9 @@ struct StepRecorder {
         if (p % 2 == 0) {
             const long long ps = m->hd, hs = (long long)m->T * m->hd;
             const long long ls = (long long)m->B * m->hkv * m->T * m->hd;
+            bool fused = false;
+            if (!batched) SLI_TRY(gemv_qkv_attn(m, l, &fused));
+            if (fused) return gemv_wo(m, l);
             SLI_TRY(batched ? b_qkv(m, l) : gemv_qkv(m, l));
             // a batch is B * hkv kv heads of one layer: sequence b owns kv heads [b*hkv, (b+1)*hkv)
             SLI_TRY(mha_launch<KT>(m->q, (const KT*)m->kc, (const KT*)m->vc, m->attn, l, 0, &m->st->pos, m->T, m->hd,
@@ -1236,6 +1284,7 @@ static int check_device_errors(sli_model* m) {
     std::string why;
     if (bits & kPsErrTimeout) why += " persistent-step barrier timed out;";
     if (bits & kOsErrTimeout) why += " one-shot all-reduce timed out (the one-shot path is now refused);";
+    if (bits & kAttnErrHand) why += " fused q/k/v + attention hand-off wait timed out;";
     return fail(SLI_ERR_STATE, "device error bits 0x" + std::to_string(bits) + ":" + why + " outputs are stale");
 }
 
@@ -1403,6 +1452,10 @@ static int create_model(const sli_model_config* cfg, const void* comm_id, sli_tp
     A((void**)&m->logits, sizeof(float) * B * m->v_n);
     A((void**)&m->part, mha_part_bytes(m->T, B * m->hq, hd));  // split-context partials
     A((void**)&m->attn_count, sizeof(unsigned) * B * m->hkv);   // per-kv-head arrival counters (kept zero)
+    if (B == 1) {
+        A((void**)&m->qa_kv, sizeof(float) * 2 * m->hkv * hd);
+        A((void**)&m->qa_count, sizeof(unsigned) * attn_hand_words(m->hkv));
+    }
     size_t bg_part = 0;
     int bg_groups = 1;
     const int cus = gemv_max_blocks();  // device_cus(), or the tests' SLI_DEBUG_GEMV_MAX_BLOCKS cap
@@ -1451,6 +1504,7 @@ static int create_model(const sli_model_config* cfg, const void* comm_id, sli_tp
         return bail(fail(SLI_ERR_HIP, "rope table upload"));
     if (hipMemset(m->prompt, 0, sizeof(int32_t) * B * (m->T + 1)) != hipSuccess ||
         hipMemset(m->attn_count, 0, sizeof(unsigned) * B * m->hkv) != hipSuccess ||
+        (m->qa_count && hipMemset(m->qa_count, 0, sizeof(unsigned) * attn_hand_words(m->hkv)) != hipSuccess) ||
         hipMemset(m->hist, 0, sizeof(int32_t) * B * (m->T + 1)) != hipSuccess ||
         (m->bg_cnt && hipMemset(m->bg_cnt, 0, sizeof(unsigned) * bg_groups) != hipSuccess))
         return bail(fail(SLI_ERR_HIP, "memset"));
@@ -1678,6 +1732,13 @@ static std::vector<PfState> pf_chunks(int n) {
 }
 
 extern "C" int sli_model_prefill_path(const sli_model* m) { return m && m->B == 1 && pf_supported(m) ? 1 : 0; }
+
+extern "C" int sli_model_fused_qkv_attn(sli_model* m) {
+    if (!m || m->B != 1 || m->exec == SLI_EXEC_PERSISTENT) return 0;
+    bool done = false;
+    if (SLI_DISPATCH(m, gemv_qkv_attn, m, 0, &done, true) != SLI_OK) return 0;
+    return done ? 1 : 0;
+}
 
 extern "C" int sli_model_prefill(sli_model* m, const int32_t* ids, int32_t n) {
     SLI_CHECK(m && ids, SLI_ERR_ARG, "null argument");

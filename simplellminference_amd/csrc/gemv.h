@@ -26,6 +26,7 @@ struct GemvIn {
     unsigned long long* stamps = nullptr;  // diagnostic (tools/gemv_lab): per-wave s_memrealtime x4
     int csplit = 1;  // column parts per unit (gemv_block): a unit's rows split over up to csplit waves
     int cw = 16;     // waves per workgroup that stream (gemv_wave_count); the others only shadow loads
+    int blk0 = 0;    // workgroups in front of the GEMV's own in the grid (qkv_attn.h: the attention's); OFFS only
 };
 
 constexpr int kGemvThreads = 1024;  // one persistent 16-wave workgroup per CU: x staged once per CU
@@ -327,7 +328,7 @@ inline size_t gemv_res_floats(int units, int grid, int R, int csplit = 1) {
 // for the first weight chunk (staged 4-6 us into a 10-30 us launch). The epilogue (residual reads,
 // RoPE, K/V writes, logits) runs once per workgroup after the loop, one thread per unit.
 // Prologue order: input loads, first weight chunk, input commit + barrier (see XStage).
-template <typename WT, int R, int U, bool NT, class Epi, class Stage, int NB = 2, bool SPLIT = false>
+template <typename WT, int R, int U, bool NT, class Epi, class Stage, int NB = 2, bool SPLIT = false, bool OFFS = false>
 __device__ __forceinline__ void gemv_block(const WT* __restrict__ W, const GemvIn& in, Epi& epi, Stage& stage,
                                            float* smem) {
     const float* xs = smem + kGemvLdsHead;
@@ -340,9 +341,11 @@ __device__ __forceinline__ void gemv_block(const WT* __restrict__ W, const GemvI
     const int nvec = in.cols / EPV;
     const size_t row_bytes = (size_t)in.cols * sizeof(WT);
     const int nunits = epi.units();
-    const int total_waves = gridDim.x * nwaves;
-    const int ub = gemv_unit_begin(blockIdx.x * nwaves, nunits, total_waves);  // workgroup's first unit
-    const int ue = gemv_unit_begin((blockIdx.x + 1) * nwaves, nunits, total_waves);
+    // OFFS: the GEMV is workgroups [in.blk0, gridDim.x) of a launch it shares (qkv_attn.h)
+    const int bx = OFFS ? (int)blockIdx.x - in.blk0 : (int)blockIdx.x;
+    const int total_waves = (OFFS ? (int)gridDim.x - in.blk0 : (int)gridDim.x) * nwaves;
+    const int ub = gemv_unit_begin(bx * nwaves, nunits, total_waves);  // workgroup's first unit
+    const int ue = gemv_unit_begin((bx + 1) * nwaves, nunits, total_waves);
     const int cpr = (nvec + CV - 1) / CV;  // chunks per row
     // Column split (small matrices, e.g. tensor-parallel shards): a unit's rows are cut into CS parts of
     // cpp chunks; the workgroup's (unit, part) items are balanced over its waves and the parts' row sums
@@ -480,7 +483,7 @@ __device__ __forceinline__ void gemv_block(const WT* __restrict__ W, const GemvI
     }
     epi.finish(smem);
     if (in.stamps && lane == 0) {
-        unsigned long long* p = in.stamps + ((size_t)blockIdx.x * nwaves + wave) * 4;
+        unsigned long long* p = in.stamps + ((size_t)bx * nwaves + wave) * 4;
         p[0] = t_entry;
         p[1] = t_staged;
         p[2] = __builtin_amdgcn_s_memrealtime();
