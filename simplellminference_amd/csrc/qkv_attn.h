@@ -130,7 +130,12 @@ hipError_t launch_qkv_attn(const WT* W, const GemvIn& in_, const EpiQKVHand<KT>&
     const int g = e.g;
     const int n_attn = a.n_kv_heads * a.max_splits;
     const int maxb = gemv_max_blocks();
-    if ((g != 1 && g != 2) || (hd != 64 && hd != 128) || 4 * n_attn > maxb || a.n_kv_heads > kGemvLdsHead)
+    // the attention's share of the grid: at most 1 / qa_div of the CUs (SLI_QKV_ATTN_DIV, default 4; A/B knob)
+    static const int qa_div = [] {
+        const char* e = getenv("SLI_QKV_ATTN_DIV");
+        return e && atoi(e) >= 2 ? atoi(e) : 4;
+    }();
+    if ((g != 1 && g != 2) || (hd != 64 && hd != 128) || qa_div * n_attn > maxb || a.n_kv_heads > kGemvLdsHead)
         return hipErrorNotSupported;
     const GemvSplit sp = gemv_split<WT, 4>(units, in_.cols);  // (CS 1 runs the split instantiation unsplit)
     if (dry) return hipSuccess;  // (sli_model_fused_qkv_attn: would launch)
