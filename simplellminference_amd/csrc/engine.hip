@@ -81,6 +81,7 @@ struct sli_model {
     unsigned* attn_count = nullptr;
     float* qa_kv = nullptr;       // batch 1: the fused q/k/v + attention launch's hand-off rows [2][hkv][hd] (qkv_attn.h)
     unsigned* qa_count = nullptr; // its per-kv-head counters (attention.h attn_hand_words; zero between launches)
+    unsigned* qa_chain = nullptr; // the chain launch's (q/k/v + attention + wo) heads-merged / wo-seen counters
     int wo_merge = 1;           // batch 1: 1 = the wo GEMV merges the attention's splits while staging its input,
                                 // 0 = the attention's last-arriving workgroup merges them (wo_merges)
     int wo_ks = 1;              // batch-1 TP-1 wo split over its columns (wo_ksplit): partials [wo_ks][D]
@@ -549,6 +550,14 @@ static bool sliced_oneshot() {
 // unset: single-rank models only (a rank process that may share its GPU with others keeps the two launches
 // unless the launcher knows each rank has a device of its own: bench.py sets 1 then). In-process groups never
 // (their ranks' launches share one device).
+// SLI_QKV_CHAIN=1: the wo GEMV joins the fused launch where it can (qkv_attn.h launch_qkv_attn_wo; A/B knob)
+static bool qkv_chain_on() {
+    static const bool on = [] {
+        const char* e = getenv("SLI_QKV_CHAIN");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
 static bool qkv_attn_on(const sli_model* m) {
     static const int env = [] {
         const char* e = getenv("SLI_QKV_ATTN");
@@ -579,9 +588,10 @@ struct StepRecorder {
         SLI_HIP((launch_gemv_u<WT, 2, 4, NT>((const WT*)w.qkv, in, e, (m->hq + 2 * m->hkv) * (m->hd / 2), m->stream)));
         return SLI_OK;
     }
-    // q/k/v + attention as one launch (qkv_attn.h) where the shape qualifies; *done = false: run the two launches
-    static int gemv_qkv_attn(sli_model* m, int l, bool* done, bool dry = false) {
-        *done = false;
+    // q/k/v + attention as one launch (qkv_attn.h) where the shape qualifies: *done = 1; with wo too (the chain,
+    // SLI_QKV_CHAIN=1): 2; 0: run the separate launches
+    static int gemv_qkv_attn(sli_model* m, int l, int* done, bool dry = false) {
+        *done = 0;
         if constexpr (std::is_same<KT, __half>::value && !std::is_same<WT, float>::value) {
             if (!m->qa_count || !qkv_attn_on(m)) return SLI_OK;
             const LayerW& w = m->layers[l];
@@ -600,11 +610,39 @@ struct StepRecorder {
             a.hand_count = m->qa_count;
             a.hand_expect = (unsigned)((g + 2) * (m->hd / 2));
             a.hand_err = &m->st->error;
+            if constexpr (std::is_same<WT, __half>::value) {
+                // the chain: wo in the same launch (plain input merged by the heads' last attention workgroups);
+                // its exchange only in the per-workgroup form (the launch-level form counts the whole grid)
+                if (qkv_chain_on() && m->qa_chain && m->wo_ks == 1 &&
+                    (!fused_ar(m) || m->ar_mode == SLI_ALLREDUCE_FUSED_WG)) {
+                    AttnArgs<KT> ac = a;
+                    ac.defer_merge = 0;
+                    ac.chain_done = m->qa_chain;
+                    unsigned* seen = m->qa_chain + kAttnHandLine;
+                    const GemvIn iw{m->attn, nullptr, 0.0f, m->hq * m->hd};
+                    const int units = (m->hq + 2 * m->hkv) * (m->hd / 2);
+                    hipError_t rc;
+                    if (fused_ar(m)) {
+                        rc = launch_qkv_attn_wo<KT>((const __half*)w.qkv, in, e, ac, units, m->hd, (const __half*)w.wo, iw,
+                                                    push_epi(m, w.wo_s, 0), m->D, m->qa_chain, seen, kOsMaxWg, m->stream, dry);
+                    } else {
+                        const bool tp = m->partial;
+                        EpiStore<1> eo{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, w.wo_s, 1.0f, m->D};
+                        rc = launch_qkv_attn_wo<KT>((const __half*)w.qkv, in, e, ac, units, m->hd, (const __half*)w.wo, iw,
+                                                    eo, m->D, m->qa_chain, seen, 1 << 30, m->stream, dry);
+                    }
+                    if (rc != hipErrorNotSupported) {
+                        SLI_HIP(rc);
+                        *done = 2;
+                        return SLI_OK;
+                    }
+                }
+            }
             const hipError_t r = launch_qkv_attn<WT, KT>((const WT*)w.qkv, in, e, a, (m->hq + 2 * m->hkv) * (m->hd / 2),
                                                          m->hd, m->stream, dry);
             if (r == hipErrorNotSupported) return SLI_OK;
             SLI_HIP(r);
-            *done = true;
+            *done = 1;
         }
         return SLI_OK;
     }
@@ -897,9 +935,10 @@ struct StepRecorder {
         if (p % 2 == 0) {
             const long long ps = m->hd, hs = (long long)m->T * m->hd;
             const long long ls = (long long)m->B * m->hkv * m->T * m->hd;
-            bool fused = false;
+            int fused = 0;
             if (!batched) SLI_TRY(gemv_qkv_attn(m, l, &fused));
-            if (fused) return gemv_wo(m, l);
+            if (fused == 2) return SLI_OK;  // wo ran in the same launch
+            if (fused == 1) return gemv_wo(m, l);
             SLI_TRY(batched ? b_qkv(m, l) : gemv_qkv(m, l));
             // a batch is B * hkv kv heads of one layer: sequence b owns kv heads [b*hkv, (b+1)*hkv)
             SLI_TRY(mha_launch<KT>(m->q, (const KT*)m->kc, (const KT*)m->vc, m->attn, l, 0, &m->st->pos, m->T, m->hd,
@@ -1455,6 +1494,7 @@ static int create_model(const sli_model_config* cfg, const void* comm_id, sli_tp
     if (B == 1) {
         A((void**)&m->qa_kv, sizeof(float) * 2 * m->hkv * hd);
         A((void**)&m->qa_count, sizeof(unsigned) * attn_hand_words(m->hkv));
+        A((void**)&m->qa_chain, sizeof(unsigned) * 2 * kAttnHandLine);
     }
     size_t bg_part = 0;
     int bg_groups = 1;
@@ -1505,6 +1545,7 @@ static int create_model(const sli_model_config* cfg, const void* comm_id, sli_tp
     if (hipMemset(m->prompt, 0, sizeof(int32_t) * B * (m->T + 1)) != hipSuccess ||
         hipMemset(m->attn_count, 0, sizeof(unsigned) * B * m->hkv) != hipSuccess ||
         (m->qa_count && hipMemset(m->qa_count, 0, sizeof(unsigned) * attn_hand_words(m->hkv)) != hipSuccess) ||
+        (m->qa_chain && hipMemset(m->qa_chain, 0, sizeof(unsigned) * 2 * kAttnHandLine) != hipSuccess) ||
         hipMemset(m->hist, 0, sizeof(int32_t) * B * (m->T + 1)) != hipSuccess ||
         (m->bg_cnt && hipMemset(m->bg_cnt, 0, sizeof(unsigned) * bg_groups) != hipSuccess))
         return bail(fail(SLI_ERR_HIP, "memset"));
@@ -1735,9 +1776,9 @@ extern "C" int sli_model_prefill_path(const sli_model* m) { return m && m->B == 
 
 extern "C" int sli_model_fused_qkv_attn(sli_model* m) {
     if (!m || m->B != 1 || m->exec == SLI_EXEC_PERSISTENT) return 0;
-    bool done = false;
+    int done = 0;
     if (SLI_DISPATCH(m, gemv_qkv_attn, m, 0, &done, true) != SLI_OK) return 0;
-    return done ? 1 : 0;
+    return done;
 }
 
 extern "C" int sli_model_prefill(sli_model* m, const int32_t* ids, int32_t n) {

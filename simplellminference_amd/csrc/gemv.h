@@ -27,6 +27,7 @@ struct GemvIn {
     int csplit = 1;  // column parts per unit (gemv_block): a unit's rows split over up to csplit waves
     int cw = 16;     // waves per workgroup that stream (gemv_wave_count); the others only shadow loads
     int blk0 = 0;    // workgroups in front of the GEMV's own in the grid (qkv_attn.h: the attention's); OFFS only
+    int blk1 = 0;    // OFFS: the end of the GEMV's workgroups (0: the grid's end)
 };
 
 constexpr int kGemvThreads = 1024;  // one persistent 16-wave workgroup per CU: x staged once per CU
@@ -51,6 +52,20 @@ constexpr int kGemvStageV4 = 4;  // float4 of x per thread: 1024 threads x 4 x 4
 template <int G>
 __device__ __forceinline__ int xswz(int f) {
     return G == 1 ? f : f ^ ((f >> 4) & (G - 1));
+}
+
+// Stages that wait for their input inside issue() (kLate = true) are issued after the first weight steps.
+template <class S, class = void>
+struct StageLate {
+    static constexpr bool value = false;
+};
+template <class S>
+struct StageLate<S, std::void_t<decltype(S::kLate)>> {
+    static constexpr bool value = S::kLate;
+};
+template <class S>
+__host__ __device__ constexpr bool stage_late() {
+    return StageLate<S>::value;
 }
 
 template <int G>
@@ -343,7 +358,7 @@ __device__ __forceinline__ void gemv_block(const WT* __restrict__ W, const GemvI
     const int nunits = epi.units();
     // OFFS: the GEMV is workgroups [in.blk0, gridDim.x) of a launch it shares (qkv_attn.h)
     const int bx = OFFS ? (int)blockIdx.x - in.blk0 : (int)blockIdx.x;
-    const int total_waves = (OFFS ? (int)gridDim.x - in.blk0 : (int)gridDim.x) * nwaves;
+    const int total_waves = (OFFS ? (in.blk1 > 0 ? in.blk1 : (int)gridDim.x) - in.blk0 : (int)gridDim.x) * nwaves;
     const int ub = gemv_unit_begin(bx * nwaves, nunits, total_waves);  // workgroup's first unit
     const int ue = gemv_unit_begin((bx + 1) * nwaves, nunits, total_waves);
     const int cpr = (nvec + CV - 1) / CV;  // chunks per row
@@ -365,7 +380,9 @@ __device__ __forceinline__ void gemv_block(const WT* __restrict__ W, const GemvI
 
     const unsigned long long t_entry = in.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
     unsigned long long t_staged = 0;
-    stage.issue(in);
+    // (a LATE stage (qkv_attn.h XStageHand) waits for its input inside issue(): it is issued after the first
+    // weight steps, so the weights stream during the wait)
+    if constexpr (!stage_late<Stage>()) stage.issue(in);
     // the epilogue's own inputs for this thread's unit (the store loop's first unit): in flight with the
     // input, landed long before the stream ends instead of a round trip after it
     const int pre_unit = max(min(ub + (int)threadIdx.x, nunits - 1), 0);
@@ -447,6 +464,7 @@ __device__ __forceinline__ void gemv_block(const WT* __restrict__ W, const GemvI
         next(lq);
     }
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (stage_late<Stage>()) stage.issue(in);
     stage.commit(smem, in);
     __syncthreads();
     epi.prefetch_b(pre_unit);

@@ -239,9 +239,10 @@ class LlamaModel:
         """'mfma' (chunked MFMA GEMMs) or 'decode' (teacher-forced decode steps): sli_model_prefill_path."""
         return "mfma" if _lib.load().sli_model_prefill_path(self._h) == 1 else "decode"
 
-    def fused_qkv_attn(self) -> bool:
-        """True when the decode step runs q/k/v + attention as one launch per layer: sli_model_fused_qkv_attn."""
-        return _lib.load().sli_model_fused_qkv_attn(self._h) == 1
+    def fused_qkv_attn(self) -> int:
+        """1 when the decode step runs q/k/v + attention as one launch per layer, 2 when wo joins it too (the chain),
+        0 otherwise: sli_model_fused_qkv_attn."""
+        return int(_lib.load().sli_model_fused_qkv_attn(self._h))
 
     def predict_prefill(self, prompt_ids, max_length: int, want_logits: bool = False):
         """predict() with the prompt prefilled; logits rows of positions < len(prompt) - 1 are NaN."""

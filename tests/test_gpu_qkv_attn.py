@@ -5,7 +5,8 @@ merge), so its results are compared BIT-exactly with the two launches on the sam
 runs in two child processes, SLI_QKV_ATTN=1 and SLI_QKV_ATTN=0 (the switch is read once per process). Cases:
 the tiny presets at TP 1 (MHA and GQA-2, head_dim 64, fp16 / int8 weights, a greedy run of 24 tokens), and one
 rank of Llama-2-7B's TP-4 / TP-8 shards (2 layers, ctx 2048, head_dim 128, 8 splits per head; SLI_DEBUG_NOCOMM:
-the rank's own step, no exchange) at positions on and around the split and wave boundaries, each step run twice
+the rank's own step, no exchange; also as the chain, wo in the same launch) at positions on and around the split
+and wave boundaries, each step run twice
 (the counters the launch leaves at zero must serve the next launch). The tiny runs are also held to the oracle
 through the TP-1 tests that run the default path (test_gpu_model.py)."""
 import json
@@ -48,11 +49,13 @@ def _child(name, w, tp, out):
         json.dump(res, f)
 
 
-def _run(tmp_path, name, w, tp, qa):
+def _run(tmp_path, name, w, tp, qa, chain=False):
     env = dict(os.environ, SLI_QKV_ATTN=str(qa))
+    if chain:
+        env["SLI_QKV_CHAIN"] = "1"
     if tp > 1:
         env["SLI_DEBUG_NOCOMM"] = "1"
-    out = str(tmp_path / f"{name.replace(':', '_')}_{w}_{tp}_{qa}")
+    out = str(tmp_path / f"{name.replace(':', '_')}_{w}_{tp}_{qa}_{int(chain)}")
     r = subprocess.run([sys.executable, os.path.abspath(__file__), name, w, str(tp), out], env=env,
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -61,13 +64,16 @@ def _run(tmp_path, name, w, tp, qa):
     return res, np.load(out + ".npy")
 
 
-@pytest.mark.parametrize("name,w,tp", [("tiny", "f16", 1), ("tiny-gqa", "f16", 1), ("tiny", "i8", 1),
-                                       ("tiny-gqa", "i8", 1), ("llama2-7b:2", "f16", 8), ("llama2-7b:2", "i8", 8),
-                                       ("llama2-7b:2", "f16", 4)])
-def test_fused_qkv_attention_matches_two_launches(gpu, tmp_path, name, w, tp):
-    fused, a = _run(tmp_path, name, w, tp, 1)
+@pytest.mark.parametrize("name,w,tp,chain", [("tiny", "f16", 1, False), ("tiny-gqa", "f16", 1, False),
+                                             ("tiny", "i8", 1, False), ("tiny-gqa", "i8", 1, False),
+                                             ("llama2-7b:2", "f16", 8, False), ("llama2-7b:2", "i8", 8, False),
+                                             ("llama2-7b:2", "f16", 4, False), ("llama2-7b:2", "f16", 8, True),
+                                             ("llama2-7b:2", "f16", 4, True)])
+def test_fused_qkv_attention_matches_two_launches(gpu, tmp_path, name, w, tp, chain):
+    """chain: wo in the same launch too (SLI_QKV_CHAIN=1, sli_model_fused_qkv_attn == 2)."""
+    fused, a = _run(tmp_path, name, w, tp, 1, chain)
     plain, b = _run(tmp_path, name, w, tp, 0)
-    assert fused["fused"] and not plain["fused"]
+    assert fused["fused"] == (2 if chain else 1) and plain["fused"] == 0
     assert fused["error"] == 0 and plain["error"] == 0
     if tp == 1:
         assert fused["toks"] == plain["toks"]

@@ -46,7 +46,7 @@ for world in [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]:
     ms = 1e3 * (time.perf_counter() - t0) / n
     what = f"all-reduces {ar} (loopback)" if ar and world > 1 else "no all-reduces"
     tag = "" if (PRESET, BATCH, CTX) == ("llama2-7b", 1, 2048) else f"{PRESET} B{BATCH} ctx {CTX} "
-    qa = " qkv+attn fused" if m.fused_qkv_attn() else ""
+    qa = {0: "", 1: " qkv+attn fused", 2: " qkv+attn+wo fused"}[m.fused_qkv_attn()]
     print(f"{tag}tp{world} rank {world - 1} [{m.exec_mode()}{qa}]: {ms:.3f} ms/step compute ({what}); device error "
           f"{m.state()['error']}", flush=True)
     m.close()
