@@ -207,7 +207,8 @@ int sli_model_prefill(sli_model* m, const int32_t* ids, int32_t n);
 int sli_model_prefill_path(const sli_model* m);
 /* 1: the batch-1 decode step runs each layer's q/k/v projection and attention as ONE launch (qkv_attn.h: the
  * attention's K/V rows below the position stream while the projection runs; q and this step's K/V row are
- * handed over inside the launch), 0: two launches (model.cpp:70-84's matmul / rope / mha sequence either way).
+ * handed over inside the launch); 2: the wo projection joins that launch too (SLI_QKV_CHAIN=1, opt-in, measured
+ * slower); 0: separate launches (model.cpp:70-84's matmul / rope / mha sequence either way).
  * Taken where the shape qualifies (heads per kv head 1 or 2, head_dim 64 / 128, fp16 K/V cache, fp16 / int8
  * weights, an attention grid of at most a quarter of the CUs) and SLI_QKV_ATTN allows it
  * (1: always; 0: never; unset: single-rank models). */
