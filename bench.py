@@ -40,8 +40,7 @@ METRIC = "decode tokens/sec, Llama-7B fp16 seq=1 ctx=2048, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 CTX = 2048
 FAMILY_KERNELS = {
-    False: {"step": "ps_step_kernel (the whole decode step as one persistent launch: 5 phases x 32 layers + LM head)",
-            "qkv": "gemv_kernel<EpiQKV> (RMSNorm + [wq;wk;wv] GEMV + RoPE + K/V write)",
+    False: {"qkv": "gemv_kernel<EpiQKV> (RMSNorm + [wq;wk;wv] GEMV + RoPE + K/V write)",
             "attention": "attn_partial_kernel (split-context flash decode + last-arriver merge)",
             "wo": "gemv_merge_kernel<EpiKPart> (attention split merge while staging + K-split wo GEMV -> 2 partial "
                   "rows; past 8 splits per head: the attention merges and wo is gemv_kernel<EpiStore>)",
@@ -64,9 +63,6 @@ def parse():
     ap.add_argument("--preset", default="llama2-7b")
     ap.add_argument("--ctx", type=int, default=CTX)
     ap.add_argument("--batch", type=int, default=1, help="sequences decoding in lockstep (MFMA projections if > 1)")
-    ap.add_argument("--exec", default="launches", choices=["launches", "persistent"],
-                    help="launches: one graph of fused launches (default, fastest measured); persistent: the whole "
-                         "step as one launch with grid barriers (batch 1, TP 1; DESIGN.md §4)")
     ap.add_argument("--tp-allreduce", default="auto", choices=["auto", "rccl", "oneshot", "fused", "fused_wg"],
                     help="TP all-reduce: auto = the one-shot exchange fused into the wo / down launches per "
                          "workgroup when every rank has its own GPU (else batch 1: one summing workgroup per launch, "
@@ -187,6 +183,18 @@ def _oneshot_opened(model, dist, torch, mode) -> bool:
     return flag.item() == 1
 
 
+def _own_gpus(dist, torch, local: int, world: int) -> bool:
+    """True when every rank drives a DIFFERENT GPU (its PCI domain / bus / device id and uuid all-gathered over
+    gloo): only then may the step use the modes whose kernels spin-wait on their own grid or on the peers (the fused
+    q/k/v + attention launch, the per-workgroup exchange). Ranks that share a device, or a torch without the PCI
+    fields, get the modes that never wait across launches."""
+    p = torch.cuda.get_device_properties(local)
+    key = ":".join(str(getattr(p, f, "?")) for f in ("pci_domain_id", "pci_bus_id", "pci_device_id", "uuid"))
+    keys = [None] * world
+    dist.all_gather_object(keys, key)
+    return "?" not in key and len(set(keys)) == world
+
+
 def progress(msg):
     """A progress line on stderr (long profiled runs stay visibly alive; stdout keeps the one JSON line)."""
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
@@ -220,14 +228,13 @@ def main():
         cid = box[0]
     cfg = preset(a.preset, max_length=a.ctx)
     B = a.batch
-    if dist_on and world <= max(1, torch.cuda.device_count()):
+    own_gpu = dist_on and _own_gpus(dist, torch, local, world)
+    if own_gpu:
         # each rank has a GPU of its own: q/k/v + attention as one launch on the shards where it fits
         # (csrc/qkv_attn.h; its attention workgroups wait inside the launch, so ranks sharing a GPU keep two launches)
         os.environ.setdefault("SLI_QKV_ATTN", "1")
     model = LlamaModel(config=cfg, w_dtype=a.w_dtype, kv_dtype="f16", tp_rank=rank, tp_size=world, comm_id=cid,
                        device=local, seed=1, batch=B).init()
-    exec_mode = a.exec
-    model.set_exec(exec_mode)
     model.fill_kv_synthetic(7, a.ctx - 1)
     for b in range(B):  # every sequence at position ctx-1 (KV rows 0..ctx-2 resident), its own token
         model.set_state_seq(b, 1234 + 17 * b, a.ctx - 1, advance=False)
@@ -244,7 +251,6 @@ def main():
         # auto: the exchange inside wo / down per workgroup (batch 1: the GEMV; batch > 1: per MFMA group) when
         # every rank has a GPU of its own (ranks sharing one would starve each other of CUs), else batch 1 through
         # one summing workgroup per launch, batch > 1 through the sliced one-shot launch
-        own_gpu = world <= max(1, torch.cuda.device_count())
         os_mode = (a.tp_allreduce if a.tp_allreduce in ("oneshot", "fused", "fused_wg")
                    else "fused_wg" if own_gpu else ("fused" if B == 1 else "oneshot"))
         if os.environ.get("SLI_DEBUG_NOCOMM") and a.tp_allreduce != "rccl":
@@ -296,16 +302,10 @@ def main():
     fam = model.time_families(a.gemv_iters)
     sfl = model.time_stream(a.gemv_iters)  # the measured streaming-read floor of the same launches
     g = model.time_gemv(a.gemv_iters)
-    if exec_mode == "persistent":
-        # the step IS one kernel (ps_step_kernel): its algorithmic bytes (all weights + the live K/V) per launch
-        dom = "step"
-        d = {"avg_us": model.time_steps(a.gemv_iters), "bytes_per_launch": wbytes + kvbytes, "launches_per_step": 1}
-        step_dev_us = d["avg_us"]
-    else:
-        # the dominant kernel: the family with the largest device time per step
-        dom = max(fam, key=lambda f: fam[f]["avg_us"] * fam[f]["launches_per_step"])
-        d = fam[dom]
-        step_dev_us = sum(f["avg_us"] * f["launches_per_step"] for f in fam.values())
+    # the dominant kernel: the family with the largest device time per step
+    dom = max(fam, key=lambda f: fam[f]["avg_us"] * fam[f]["launches_per_step"])
+    d = fam[dom]
+    step_dev_us = sum(f["avg_us"] * f["launches_per_step"] for f in fam.values())
     achieved = d["bytes_per_launch"] / (d["avg_us"] * 1e-6) / 1e9
 
     # a true greedy decode beside the idempotent-step timing: 64 tokens at positions ctx-64 .. ctx-1, the
@@ -362,7 +362,7 @@ def main():
                    "step_bytes_per_gpu": round(wbytes + kvbytes),
                    "hbm_roofline_tokens_per_s": round(B * HBM_PEAK_GBS * 1e9 / (wbytes + kvbytes), 1),
                    "step_frac_of_hbm_peak": round((wbytes + kvbytes) / (ms * 1e-3) / (HBM_PEAK_GBS * 1e9), 4)},
-        "exec": exec_mode,
+        "exec": "launches",
         "tp_allreduce": allreduce,
         "qkv_attn_fused": model.fused_qkv_attn(),
         "roofline": {"bound": "hbm", "kernel": f"{dom}: {FAMILY_KERNELS[B > 1][dom]}",
@@ -375,9 +375,7 @@ def main():
                      "frac_of_stream": round(sfl[dom] / d["avg_us"], 4) if dom in sfl else None,
                      "launches_per_step": d["launches_per_step"],
                      "share_of_step_device_time": round(d["avg_us"] * d["launches_per_step"] / step_dev_us, 4),
-                     "families_note": ("per-family timing of the launch path's kernels (the same arithmetic; "
-                                       "the one-launch step runs them as ops of one launch)"
-                                       if exec_mode != "launches" else "the step's launches by family"),
+                     "families_note": "the step's launches by family",
                      "families": {f: {"avg_launch_us": round(v["avg_us"], 3),
                                       "bytes_per_launch": round(v["bytes_per_launch"]),
                                       "launches_per_step": v["launches_per_step"],

@@ -219,12 +219,10 @@ int sli_model_predict_prefill(sli_model* m, const int32_t* prompt, int32_t n_pro
                               int32_t* tokens_out, float* logits_out);
 /* The tokens fed at positions [0, n) of sequence seq. */
 int sli_model_get_history(sli_model* m, int32_t seq, int32_t n, int32_t* out);
-/* Execution of the step (the graph is re-captured on the next step after a change):
- *  SLI_EXEC_LAUNCHES   one hipGraph of ~5 fused launches per layer (every configuration);
- *  SLI_EXEC_PERSISTENT the whole step as ONE persistent launch (one workgroup per CU, grid barriers between
- *                      phases, the next phase's weights streamed before each barrier): batch 1, no tensor
- *                      parallelism, 1 or 2 heads per kv head; SLI_ERR_STATE otherwise. */
-enum { SLI_EXEC_LAUNCHES = 0, SLI_EXEC_PERSISTENT = 1 };
+/* Execution of the step: SLI_EXEC_LAUNCHES, one hipGraph of ~5 fused launches per layer (every configuration).
+ * (Round 5 removed the opt-in persistent one-launch step, mode 1: measured slower every round, DESIGN.md §9;
+ * sli_model_set_exec(1) returns SLI_ERR_ARG.) */
+enum { SLI_EXEC_LAUNCHES = 0 };
 int sli_model_set_exec(sli_model* m, int32_t mode);
 int sli_model_get_exec(sli_model* m, int32_t* mode);
 /* One decode step (hipGraph replay; captured on first use). Asynchronous on the model's stream. */
@@ -281,12 +279,7 @@ int sli_tp_group_predict_prefill(sli_tp_group* g, const int32_t* prompt, int32_t
  * the launches per step. */
 int sli_model_time_gemv(sli_model* m, int32_t iters, double* avg_us, double* bytes_per_launch,
                         int32_t* launches_per_step);
-/* Diagnostic: one persistent step with in-kernel s_memrealtime stamps (100 MHz): host[(p * grid + wg) * 5 + k]
- * for phase p of 2 + 5L (embedding; qkv, attention, wo, gate/up, down per layer; LM head), workgroup wg,
- * k = entry, barrier passed, input staged, compute done, arrival. n = (2 + 5L) * grid * 5. */
-int sli_model_ps_stamps(sli_model* m, uint64_t* host, int64_t n, int32_t* grid);
-/* Device time of one replayed step: `iters` graph launches between HIP events on the model's stream (in
- * SLI_EXEC_PERSISTENT mode: one memset node + the one persistent launch). */
+/* Device time of one replayed step: `iters` graph launches between HIP events on the model's stream. */
 int sli_model_time_steps(sli_model* m, int32_t iters, double* avg_us);
 /* Per-kernel-family probe: for each family f (sli_kernel_family) replays that family's launches of one
  * step `iters` times between HIP events on the model's stream; us[f] = mean device time per launch,

@@ -105,7 +105,6 @@ _SIGS = {
     "sli_model_stream": (c_int, [c_vp, ctypes.POINTER(c_vp)]),
     "sli_model_step_bytes": (c_int, [c_vp, P_d, P_d]),
     "sli_model_time_gemv": (c_int, [c_vp, c_i32, P_d, P_d, P_i32]),
-    "sli_model_ps_stamps": (c_int, [c_vp, c_vp, c_i64, P_i32]),
     "sli_model_comm_handle_bytes": (c_int, []),
     "sli_model_comm_handle": (c_int, [c_vp, c_vp, c_i32]),
     "sli_model_comm_open": (c_int, [c_vp, c_vp, c_i32]),

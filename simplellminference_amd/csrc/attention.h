@@ -49,10 +49,9 @@ struct AttnArgs {
                                      // per 128-byte line), then live workgroups done per kv head (the last resets)
     unsigned hand_expect = 0;        // units per kv head: (G + 2) * hd / 2
     int* hand_err = nullptr;         // DevState::error: a bounded wait that gave up sets kAttnErrHand
-    unsigned* chain_done = nullptr;  // qkv_attn.h chain: kv heads merged (the wo workgroups of the launch wait for all)
 };
 
-constexpr int kAttnErrHand = 8;               // DevState::error bit (persist.h 2, oneshot.h 4)
+constexpr int kAttnErrHand = 8;               // DevState::error bit (oneshot.h 4)
 constexpr unsigned kAttnHandSpin = 1u << 22;  // bounded wait (~seconds)
 // A kv head's arrivals are spread over kAttnHandSub counters on separate 128-byte lines (producer workgroup b
 // adds to counter b % kAttnHandSub): same-line device-scope atomics serialise (measured: one add per q/k/v unit on

@@ -449,12 +449,11 @@ struct BgEpiQKV {
     int hq, hkv, hd, T;
     int kv_seq = 1;  // 1: sequence b owns cache heads [b*hkv, (b+1)*hkv); 0: one cache shared by every lane
                      // (prefill lanes of one sequence at consecutive positions)
-    int prefetch = 1;  // 0: no epilogue prefetch (A/B: SLI_BG_EPI_PREFETCH=0)
     int p_t = -1, p_i = 0, p_b = 0, p_pos = 0;  // the prefetched item: its position, then its RoPE row
     float p_sin = 0.0f, p_cos = 0.0f;
     __device__ void pre_a(int t0, int ntg, int B) {
         const int it = threadIdx.x;
-        if (!prefetch || it >= ntg * 64 || (it & 7) >= B) return;
+        if (it >= ntg * 64 || (it & 7) >= B) return;
         p_t = t0 + (it >> 6);
         p_i = (it >> 3) & 7;
         p_b = it & 7;

@@ -30,7 +30,6 @@
 #include "gemv.h"
 #include "oneshot.h"
 #include "ops_internal.h"
-#include "persist.h"
 #include "prefill.h"
 #include "qkv_attn.h"
 #include "rope_table.h"
@@ -81,7 +80,6 @@ struct sli_model {
     unsigned* attn_count = nullptr;
     float* qa_kv = nullptr;       // batch 1: the fused q/k/v + attention launch's hand-off rows [2][hkv][hd] (qkv_attn.h)
     unsigned* qa_count = nullptr; // its per-kv-head counters (attention.h attn_hand_words; zero between launches)
-    unsigned* qa_chain = nullptr; // the chain launch's (q/k/v + attention + wo) heads-merged / wo-seen counters
     int wo_merge = 1;           // batch 1: 1 = the wo GEMV merges the attention's splits while staging its input,
                                 // 0 = the attention's last-arriving workgroup merges them (wo_merges)
     int wo_ks = 1;              // batch-1 TP-1 wo split over its columns (wo_ksplit): partials [wo_ks][D]
@@ -123,13 +121,7 @@ struct sli_model {
     bool os_loopback = false;                // debug: SLI_DEBUG_OS_LOOPBACK (oneshot.h OneShotArgs::loopback)
     char** os_peer_tab = nullptr;            // device copy of os_peer (oneshot.h EpiPush::peer_tab)
     size_t os_bytes = 0;
-    // SLI_EXEC_PERSISTENT (persist.h): the whole step as one launch
     int exec = SLI_EXEC_LAUNCHES;
-    sli::PsArgs* ps_args = nullptr;  // device copy of the args record
-    unsigned* ps_sync = nullptr;     // barrier + merge counters, zeroed by a memset node before each launch
-    size_t ps_sync_bytes = 0;
-    size_t ps_lds = 0;
-    int ps_grid = 0;
 };
 
 // In-process tensor parallelism (the "fake communicator"): tp_size rank models on
@@ -164,92 +156,7 @@ static int model_alloc(sli_model* m, void** p, size_t bytes) {
         if (rc_ != SLI_OK) return rc_;  \
     } while (0)
 
-// ---------------------------------------------------------------- persistent step (persist.h)
-static int ps_launch_model(sli_model* m, bool prepare) {
-    PsArgs a{};
-    a.hd = m->hd;
-    a.hq = m->hq;
-    a.hkv = m->hkv;
-    return ps_launch(a, m->ps_args, m->c.w_dtype, m->c.kv_dtype, m->ps_grid, m->ps_lds, m->stream, prepare);
-}
 
-// Allocate the hand-off buffers and the args record of the persistent step (once per model).
-static int ps_setup(sli_model* m) {
-    if (m->ps_args) return SLI_OK;
-    SLI_CHECK(m->B == 1, SLI_ERR_STATE, "persistent step: batch 1 only (batched decode runs the MFMA launches)");
-    SLI_CHECK(!m->partial && !m->group, SLI_ERR_STATE, "persistent step: tensor parallelism runs the launches");
-    const int g = m->hq / m->hkv;
-    SLI_CHECK(g == 1 || g == 2, SLI_ERR_STATE, "persistent step: heads per kv head must be 1 or 2");
-    const int L = m->L, D = m->D, hd = m->hd;
-    const int splits = ps_max_splits(m->c.kv_dtype, hd, m->T);
-    PsArgs a{};
-    int rc = SLI_OK;
-    auto A = [&](void** p, size_t bytes) {
-        if (rc == SLI_OK) rc = model_alloc(m, p, bytes);
-    };
-    m->ps_sync_bytes = (sizeof(unsigned) * (size_t)(kPsSyncHeads + L * m->hkv) + 15) & ~(size_t)15;
-    A((void**)&m->ps_sync, m->ps_sync_bytes);
-    A((void**)&a.xv, sizeof(float) * (size_t)(2 * L + 1) * D);
-    A((void**)&a.qv, sizeof(float) * (size_t)L * m->hq * hd);
-    A((void**)&a.kvn, sizeof(float) * (size_t)L * 2 * m->hkv * hd);
-    A((void**)&a.part, sizeof(float) * (size_t)L * m->hq * splits * (hd + kAttnPartPad));
-    A((void**)&a.attn, sizeof(float) * (size_t)L * m->hq * hd);
-    A((void**)&a.actv, sizeof(float) * (size_t)L * m->Il);
-    m->ps_grid = device_cus();
-    A((void**)&a.keys, sizeof(unsigned long long) * m->ps_grid);
-    PsLayer* layers = nullptr;
-    A((void**)&layers, sizeof(PsLayer) * L);
-    PsArgs* dev = nullptr;
-    A((void**)&dev, sizeof(PsArgs));
-    if (rc != SLI_OK) return rc;
-    std::vector<PsLayer> hl(L);
-    for (int l = 0; l < L; ++l) {
-        const LayerW& w = m->layers[l];
-        hl[l] = PsLayer{w.qkv, w.qkv_s, w.wo, w.wo_s, w.gu, w.gu_s, w.down, w.down_s};
-    }
-    a.layers = layers;
-    a.emb = m->emb;
-    a.emb_s = m->emb_s;
-    a.norms = m->norms;
-    a.kc = m->kc;
-    a.vc = m->vc;
-    a.sin_t = m->sin_t;
-    a.cos_t = m->cos_t;
-    a.st = m->st;
-    a.prompt = m->prompt;
-    a.hist = m->hist;
-    a.logits = m->logits;
-    a.sync = m->ps_sync;
-    a.D = D;
-    a.L = L;
-    a.T = m->T;
-    a.hd = hd;
-    a.hq = m->hq;
-    a.hkv = m->hkv;
-    a.Il = m->Il;
-    a.V = m->V;
-    a.v_lo = m->v_lo;
-    a.v_n = m->v_n;
-    a.max_splits = splits;
-    a.eps = m->c.eps;
-    a.scale = 1.0f / sqrtf((float)hd);  // mha_kernel.cpp:41
-    a.act_mode = m->c.act_mode;
-    SLI_HIP(hipMemcpy(layers, hl.data(), sizeof(PsLayer) * L, hipMemcpyHostToDevice));
-    SLI_HIP(hipMemcpy(dev, &a, sizeof(PsArgs), hipMemcpyHostToDevice));
-    SLI_HIP(hipMemset(m->ps_sync, 0, m->ps_sync_bytes));
-    // LDS: the staged input (the widest phase input), the per-unit results, the reduction scratch; at
-    // least kPsMinLds so that no two workgroups share a CU
-    const int max_cols = std::max(std::max(D, m->Il), m->hq * hd);
-    const int max_units = std::max(std::max((m->hq + 2 * m->hkv) * hd / 2, std::max(D, m->Il)), (m->v_n + 1) / 2);
-    const size_t need =
-        sizeof(float) * ((size_t)kGemvLdsHead + max_cols + 2 * ((size_t)max_units / m->ps_grid + 2) + D + 4);
-    m->ps_lds = std::max(kPsMinLds, (need + 255) & ~(size_t)255);
-    SLI_CHECK(m->ps_lds <= 160 * 1024, SLI_ERR_SHAPE, "persistent step: LDS image exceeds 160 KiB");
-    a.wslot = (int)(m->ps_lds / sizeof(float)) - ((D + 3) & ~3);
-    SLI_HIP(hipMemcpy(dev, &a, sizeof(PsArgs), hipMemcpyHostToDevice));
-    m->ps_args = dev;
-    return ps_launch_model(m, true);
-}
 
 #define SLI_NCCL(expr)                                                                          \
     do {                                                                                        \
@@ -527,37 +434,10 @@ __global__ void group_finalize_kernel(GroupKeyArgs a) {
 // launch_gemv_u / gemv_split: gemv.h (shared with the op-level sli_matmul)
 
 
-// batched decode: the attention's split merge as its own launch (attention.h attn_merge_kernel, mode 2);
-// SLI_BG_EPI_PREFETCH=0: the batched q/k/v epilogue loads its position and RoPE row after the stream (A/B)
-static bool bg_epi_prefetch() {
-    static const bool v = [] {
-        const char* e = getenv("SLI_BG_EPI_PREFETCH");
-        return !(e && e[0] == '0');
-    }();
-    return v;
-}
-
-// SLI_ONESHOT_SLICED=0: the separate one-shot residual sum in one workgroup (A/B measurement)
-static bool sliced_oneshot() {
-    static const bool v = [] {
-        const char* e = getenv("SLI_ONESHOT_SLICED");
-        return !(e && e[0] == '0');
-    }();
-    return v;
-}
-
 // The fused q/k/v + attention launch (qkv_attn.h). SLI_QKV_ATTN=1: wherever the shape qualifies; 0: never;
 // unset: single-rank models only (a rank process that may share its GPU with others keeps the two launches
 // unless the launcher knows each rank has a device of its own: bench.py sets 1 then). In-process groups never
 // (their ranks' launches share one device).
-// SLI_QKV_CHAIN=1: the wo GEMV joins the fused launch where it can (qkv_attn.h launch_qkv_attn_wo; A/B knob)
-static bool qkv_chain_on() {
-    static const bool on = [] {
-        const char* e = getenv("SLI_QKV_CHAIN");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
 static bool qkv_attn_on(const sli_model* m) {
     static const int env = [] {
         const char* e = getenv("SLI_QKV_ATTN");
@@ -567,14 +447,11 @@ static bool qkv_attn_on(const sli_model* m) {
     return env == 1 || !m->partial;
 }
 
-// SLI_ATTN_MERGE_LAUNCH=0 keeps the last-arriver merge inside the attention launch (A/B measurement)
-static int defer_batched() {
-    static const int v = [] {
-        const char* e = getenv("SLI_ATTN_MERGE_LAUNCH");
-        return e && e[0] == '0' ? 0 : 2;
-    }();
-    return v;
-}
+// Batched decode: the register-staged attention (fp32 cache) leaves its split merge to attn_merge_kernel (its
+// 1024 C4 workgroups run in two residency rounds, so a last-arriver merge inside the launch waits on the second
+// round: profiles/r4_c4_merge_launch_ab.txt); the MFMA attention (fp16 cache) merges inside its one resident
+// round (ops.hip attn_mfma_launch).
+constexpr int kDeferBatched = 2;
 
 template <typename WT, typename KT>
 struct StepRecorder {
@@ -588,8 +465,7 @@ struct StepRecorder {
         SLI_HIP((launch_gemv_u<WT, 2, 4, NT>((const WT*)w.qkv, in, e, (m->hq + 2 * m->hkv) * (m->hd / 2), m->stream)));
         return SLI_OK;
     }
-    // q/k/v + attention as one launch (qkv_attn.h) where the shape qualifies: *done = 1; with wo too (the chain,
-    // SLI_QKV_CHAIN=1): 2; 0: run the separate launches
+    // q/k/v + attention as one launch (qkv_attn.h) where the shape qualifies: *done = 1; 0: run the separate launches
     static int gemv_qkv_attn(sli_model* m, int l, int* done, bool dry = false) {
         *done = 0;
         if constexpr (std::is_same<KT, __half>::value && !std::is_same<WT, float>::value) {
@@ -610,34 +486,6 @@ struct StepRecorder {
             a.hand_count = m->qa_count;
             a.hand_expect = (unsigned)((g + 2) * (m->hd / 2));
             a.hand_err = &m->st->error;
-            if constexpr (std::is_same<WT, __half>::value) {
-                // the chain: wo in the same launch (plain input merged by the heads' last attention workgroups);
-                // its exchange only in the per-workgroup form (the launch-level form counts the whole grid)
-                if (qkv_chain_on() && m->qa_chain && m->wo_ks == 1 &&
-                    (!fused_ar(m) || m->ar_mode == SLI_ALLREDUCE_FUSED_WG)) {
-                    AttnArgs<KT> ac = a;
-                    ac.defer_merge = 0;
-                    ac.chain_done = m->qa_chain;
-                    unsigned* seen = m->qa_chain + kAttnHandLine;
-                    const GemvIn iw{m->attn, nullptr, 0.0f, m->hq * m->hd};
-                    const int units = (m->hq + 2 * m->hkv) * (m->hd / 2);
-                    hipError_t rc;
-                    if (fused_ar(m)) {
-                        rc = launch_qkv_attn_wo<KT>((const __half*)w.qkv, in, e, ac, units, m->hd, (const __half*)w.wo, iw,
-                                                    push_epi(m, w.wo_s, 0), m->D, m->qa_chain, seen, kOsMaxWg, m->stream, dry);
-                    } else {
-                        const bool tp = m->partial;
-                        EpiStore<1> eo{tp ? m->xpart : m->x, (!tp || m->c.tp_rank == 0) ? m->x : nullptr, w.wo_s, 1.0f, m->D};
-                        rc = launch_qkv_attn_wo<KT>((const __half*)w.qkv, in, e, ac, units, m->hd, (const __half*)w.wo, iw,
-                                                    eo, m->D, m->qa_chain, seen, 1 << 30, m->stream, dry);
-                    }
-                    if (rc != hipErrorNotSupported) {
-                        SLI_HIP(rc);
-                        *done = 2;
-                        return SLI_OK;
-                    }
-                }
-            }
             const hipError_t r = launch_qkv_attn<WT, KT>((const WT*)w.qkv, in, e, a, (m->hq + 2 * m->hkv) * (m->hd / 2),
                                                          m->hd, m->stream, dry);
             if (r == hipErrorNotSupported) return SLI_OK;
@@ -803,11 +651,9 @@ struct StepRecorder {
         a.loopback = m->os_loopback;
         if (max_u64)  // the argmax keys: 2 * B u64s, one workgroup
             hipLaunchKernelGGL(oneshot_kernel<1>, dim3(1), dim3(1024), 0, m->stream, a);
-        else if (sliced_oneshot())  // the residual sums: sliced over kOsSliceWgs workgroups
+        else  // the residual sums: sliced over kOsSliceWgs workgroups
             hipLaunchKernelGGL(oneshot_sliced_kernel, dim3(std::min(kOsSliceWgs, std::max(1, n / 64))), dim3(256), 0,
                                m->stream, a, m->os_peer_tab, m->os_wg_epoch);
-        else
-            hipLaunchKernelGGL(oneshot_kernel<0>, dim3(1), dim3(1024), 0, m->stream, a);
         SLI_HIP(hipGetLastError());
         return SLI_OK;
     }
@@ -863,7 +709,6 @@ struct StepRecorder {
         const size_t lay = (size_t)l * m->B * m->hkv * m->T * m->hd;
         BgEpiQKV<KT> e{m->q, (KT*)m->kc + lay, (KT*)m->vc + lay, &m->st->pos, kPosStride, m->sin_t, m->cos_t,
                        m->hq, m->hkv, m->hd, m->T};
-        e.prefetch = bg_epi_prefetch() ? 1 : 0;
         return bg(m, m->bg_tiled ? m->layers[l].qkv_t : m->layers[l].qkv, bin(m, m->x, m->norms + (size_t)(2 * l) * m->D, m->D), e, m->bp_qkv);
     }
     // batched wo / down with the exchange per group (oneshot.h BgEpiPush; region 3: wo, 4: down)
@@ -937,13 +782,12 @@ struct StepRecorder {
             const long long ls = (long long)m->B * m->hkv * m->T * m->hd;
             int fused = 0;
             if (!batched) SLI_TRY(gemv_qkv_attn(m, l, &fused));
-            if (fused == 2) return SLI_OK;  // wo ran in the same launch
             if (fused == 1) return gemv_wo(m, l);
             SLI_TRY(batched ? b_qkv(m, l) : gemv_qkv(m, l));
             // a batch is B * hkv kv heads of one layer: sequence b owns kv heads [b*hkv, (b+1)*hkv)
             SLI_TRY(mha_launch<KT>(m->q, (const KT*)m->kc, (const KT*)m->vc, m->attn, l, 0, &m->st->pos, m->T, m->hd,
                                    m->B * m->hq, m->B * m->hkv, ps, hs, ls, m->part, m->attn_count, s,
-                                   batched ? m->hkv : 0, batched ? kPosStride : 0, 0, batched ? defer_batched() : m->wo_merge));
+                                   batched ? m->hkv : 0, batched ? kPosStride : 0, 0, batched ? kDeferBatched : m->wo_merge));
             return batched ? b_wo(m, l) : gemv_wo(m, l);
         }
         SLI_TRY(batched ? b_gu(m, l) : gemv_gu(m, l));
@@ -984,10 +828,6 @@ struct StepRecorder {
 
     // one model and its own communicator (none, RCCL, or the debug modes)
     static int record(sli_model* m) {
-        if (m->exec == SLI_EXEC_PERSISTENT) {
-            SLI_HIP(hipMemsetAsync(m->ps_sync, 0, m->ps_sync_bytes, m->stream));
-            return ps_launch_model(m, false);
-        }
         for (int p = 0; p < 2 * m->L; ++p) {
             SLI_TRY(record_phase(m, p));
             SLI_TRY(allreduce_x(m));
@@ -1200,7 +1040,7 @@ struct StepRecorder {
                     SLI_TRY(mha_launch<KT>(m->q, (const KT*)m->kc, (const KT*)m->vc, m->attn, l, 0, &m->st->pos, m->T,
                                            m->hd, m->B * m->hq, m->B * m->hkv, ps, hs, ls, m->part, m->attn_count,
                                            m->stream, batched ? m->hkv : 0, batched ? kPosStride : 0, 0,
-                                           batched ? defer_batched() : m->wo_merge));
+                                           batched ? kDeferBatched : m->wo_merge));
                     break;
                 }
                 case SLI_FAM_WO: SLI_TRY(batched ? b_wo(m, l) : gemv_wo(m, l)); break;
@@ -1288,12 +1128,11 @@ static int capture(sli_model* m) {
     return capture_graph(m->stream, m->graph, m->graph_exec, [&]() { return SLI_DISPATCH(m, record, m); });
 }
 
+// The ranks share the group's stream, so a tile rebuild (bg_sync_tiles, only after a weight was placed) is ordered
+// after any group graph still running on it and before the next one; nothing to wait for on a plain step.
 static int capture_group(sli_tp_group* g) {
     sli_model* m0 = g->ranks[0];
-    for (sli_model* r : g->ranks) {
-        SLI_TRY(bg_sync_tiles(r));
-        SLI_HIP(hipStreamSynchronize(r->stream));
-    }
+    for (sli_model* r : g->ranks) SLI_TRY(bg_sync_tiles(r));
     return capture_graph(g->stream, g->graph, g->exec, [&]() { return SLI_DISPATCH(m0, record_group, g); });
 }
 
@@ -1310,8 +1149,8 @@ static int download_states(sli_model* m, std::vector<DevState>& h) {
     return SLI_OK;
 }
 
-// Device-side error bits (DevState::error: a bounded spin of the persistent step or of the one-shot
-// all-reduce gave up, leaving stale outputs) surfaced as a status: every predict path calls this after its
+// Device-side error bits (DevState::error: a bounded spin of the one-shot all-reduce or of the fused q/k/v +
+// attention hand-off gave up, leaving stale outputs) surfaced as a status: every predict path calls this after its
 // final stream sync, so a step that returned early never yields SLI_OK with garbage tokens.
 static int check_device_errors(sli_model* m) {
     std::vector<DevState> h;
@@ -1320,8 +1159,14 @@ static int check_device_errors(sli_model* m) {
     for (const DevState& d : h) bits |= d.error;
     if (bits == 0) return SLI_OK;
     if (bits & kOsErrTimeout) m->os_dead = true;  // epochs may disagree across ranks from here on
+    if (bits & kAttnErrHand) {
+        // a hand-off wait gave up: late q/k/v workgroups may have added their counts after the head's last attention
+        // workgroup reset them, and the next step's waits would pass early on that residue. Start them from zero.
+        if (m->qa_count) (void)hipMemsetAsync(m->qa_count, 0, sizeof(unsigned) * attn_hand_words(m->hkv), m->stream);
+        (void)hipMemsetAsync(m->attn_count, 0, sizeof(unsigned) * m->B * m->hkv, m->stream);
+        (void)hipStreamSynchronize(m->stream);
+    }
     std::string why;
-    if (bits & kPsErrTimeout) why += " persistent-step barrier timed out;";
     if (bits & kOsErrTimeout) why += " one-shot all-reduce timed out (the one-shot path is now refused);";
     if (bits & kAttnErrHand) why += " fused q/k/v + attention hand-off wait timed out;";
     return fail(SLI_ERR_STATE, "device error bits 0x" + std::to_string(bits) + ":" + why + " outputs are stale");
@@ -1392,6 +1237,40 @@ static int wo_ksplit(const sli_model* m) {
     const int epv = 16 / (int)m->wbytes;  // weight elements per 16-byte vector
     if (cols % epv || cols % 4 || sli::gemv_ksplit_grid(m->D, ks) == 0) return 1;
     return ks;
+}
+
+// The batched projections' fragment-layout weight copies (bgemm.h BgIn::tiled: one contiguous KiB per wave load;
+// C4 1742 -> 1988 tok/s, profiles/r4_bg_tiled_ab.txt). They double the projection weights in HBM (C4: +15 GB), so
+// they are allocated last and only when they fit beside everything else with 1 GiB to spare; otherwise (or if an
+// allocation fails) the model keeps streaming the row-major matrices (16 rows x 64 B per wave load), which is
+// correct, only slower. SLI_DEBUG_BG_ROWMAJOR=1 forces that fallback (tests).
+static void bg_alloc_tiles(sli_model* m) {
+    m->bg_tiled = false;
+    if (m->c.w_dtype != SLI_DT_F16 || std::getenv("SLI_DEBUG_BG_ROWMAJOR")) return;
+    const int D = m->D, QD = m->hq * m->hd;
+    std::vector<std::pair<void**, size_t>> want;
+    for (auto& w : m->layers) {
+        want.push_back({&w.qkv_t, bg_tiled_bytes(m->bp_qkv.ntiles, D)});
+        want.push_back({&w.wo_t, bg_tiled_bytes(m->bp_wo.ntiles, QD)});
+        want.push_back({&w.gu_t, bg_tiled_bytes(m->bp_gu.ntiles, D)});
+        want.push_back({&w.down_t, bg_tiled_bytes(m->bp_down.ntiles, m->Il)});
+    }
+    want.push_back({&m->lm_t, bg_tiled_bytes(m->bp_lm.ntiles, D)});
+    size_t need = 0, free_b = 0, total_b = 0;
+    for (const auto& p : want) need += p.second;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b < need + ((size_t)1 << 30)) return;
+    const size_t n0 = m->allocs.size();
+    for (const auto& p : want) {
+        if (hipMalloc(p.first, p.second) != hipSuccess) {  // undo: free the copies made so far, stay row-major
+            (void)hipGetLastError();
+            for (size_t i = n0; i < m->allocs.size(); ++i) (void)hipFree(m->allocs[i]);
+            m->allocs.resize(n0);
+            for (const auto& q : want) *q.first = nullptr;
+            return;
+        }
+        m->allocs.push_back(*p.first);
+    }
+    m->bg_tiled = true;
 }
 
 static int create_model(const sli_model_config* cfg, const void* comm_id, sli_tp_group* group, sli_model** out) {
@@ -1494,7 +1373,6 @@ static int create_model(const sli_model_config* cfg, const void* comm_id, sli_tp
     if (B == 1) {
         A((void**)&m->qa_kv, sizeof(float) * 2 * m->hkv * hd);
         A((void**)&m->qa_count, sizeof(unsigned) * attn_hand_words(m->hkv));
-        A((void**)&m->qa_chain, sizeof(unsigned) * 2 * kAttnHandLine);
     }
     size_t bg_part = 0;
     int bg_groups = 1;
@@ -1513,18 +1391,6 @@ static int create_model(const sli_model_config* cfg, const void* comm_id, sli_tp
         }
         m->key_ld = std::max(m->key_ld, m->bp_lm.groups);
         A((void**)&m->bg_ws, bg_part + 256);
-        // the fragment-layout copies (SLI_BG_TILED=0: stream the row-major matrices, 16 rows x 64 B per wave load)
-        const char* te = getenv("SLI_BG_TILED");
-        m->bg_tiled = !(te && te[0] == '0') && c.w_dtype == SLI_DT_F16;
-        if (m->bg_tiled) {
-            for (auto& w : m->layers) {
-                A(&w.qkv_t, bg_tiled_bytes(m->bp_qkv.ntiles, D));
-                A(&w.wo_t, bg_tiled_bytes(m->bp_wo.ntiles, m->hq * hd));
-                A(&w.gu_t, bg_tiled_bytes(m->bp_gu.ntiles, D));
-                A(&w.down_t, bg_tiled_bytes(m->bp_down.ntiles, m->Il));
-            }
-            A(&m->lm_t, bg_tiled_bytes(m->bp_lm.ntiles, D));
-        }
         A((void**)&m->bg_cnt, sizeof(unsigned) * bg_groups);
     }
     A((void**)&m->bkeys, sizeof(unsigned long long) * B);
@@ -1536,6 +1402,7 @@ static int create_model(const sli_model_config* cfg, const void* comm_id, sli_tp
     A((void**)&m->prompt, sizeof(int32_t) * B * (m->T + 1));
     A((void**)&m->hist, sizeof(int32_t) * B * (m->T + 1));
     if (rc != SLI_OK) return bail(rc);
+    if (B > 1) bg_alloc_tiles(m);
 
     std::vector<float> s, co;
     rope_table_host(hd, m->T, c.theta, s, co);  // rope_kernel.cpp:4-19, model.cpp:309-316
@@ -1545,7 +1412,6 @@ static int create_model(const sli_model_config* cfg, const void* comm_id, sli_tp
     if (hipMemset(m->prompt, 0, sizeof(int32_t) * B * (m->T + 1)) != hipSuccess ||
         hipMemset(m->attn_count, 0, sizeof(unsigned) * B * m->hkv) != hipSuccess ||
         (m->qa_count && hipMemset(m->qa_count, 0, sizeof(unsigned) * attn_hand_words(m->hkv)) != hipSuccess) ||
-        (m->qa_chain && hipMemset(m->qa_chain, 0, sizeof(unsigned) * 2 * kAttnHandLine) != hipSuccess) ||
         hipMemset(m->hist, 0, sizeof(int32_t) * B * (m->T + 1)) != hipSuccess ||
         (m->bg_cnt && hipMemset(m->bg_cnt, 0, sizeof(unsigned) * bg_groups) != hipSuccess))
         return bail(fail(SLI_ERR_HIP, "memset"));
@@ -1775,7 +1641,7 @@ static std::vector<PfState> pf_chunks(int n) {
 extern "C" int sli_model_prefill_path(const sli_model* m) { return m && m->B == 1 && pf_supported(m) ? 1 : 0; }
 
 extern "C" int sli_model_fused_qkv_attn(sli_model* m) {
-    if (!m || m->B != 1 || m->exec == SLI_EXEC_PERSISTENT) return 0;
+    if (!m || m->B != 1) return 0;
     int done = 0;
     if (SLI_DISPATCH(m, gemv_qkv_attn, m, 0, &done, true) != SLI_OK) return 0;
     return done;
@@ -1903,9 +1769,9 @@ int sli_model_get_history(sli_model* m, int32_t seq, int32_t n, int32_t* out) {
 
 int sli_model_set_exec(sli_model* m, int32_t mode) {
     SLI_CHECK(m, SLI_ERR_ARG, "null model");
-    SLI_CHECK(mode == SLI_EXEC_LAUNCHES || mode == SLI_EXEC_PERSISTENT, SLI_ERR_ARG, "unknown execution mode");
+    SLI_CHECK(mode == SLI_EXEC_LAUNCHES, SLI_ERR_ARG,
+              "unknown execution mode (the persistent one-launch step was removed in round 5: DESIGN.md §9)");
     SLI_HIP(hipSetDevice(m->c.device));
-    if (mode == SLI_EXEC_PERSISTENT) SLI_TRY(ps_setup(m));
     if (mode != m->exec) {  // re-capture the step graph on the next step
         SLI_HIP(hipStreamSynchronize(m->stream));
         if (m->graph_exec) (void)hipGraphExecDestroy(m->graph_exec);
@@ -2070,36 +1936,6 @@ int sli_model_step_bytes(sli_model* m, double* weight_bytes, double* kv_bytes) {
     double ctx = 0.0;
     for (const DevState& d : h) ctx += d.pos + 1.0;
     if (kv_bytes) *kv_bytes = 2.0 * m->L * ctx * m->hkv * hd * (double)m->kvbytes;
-    return SLI_OK;
-}
-
-int sli_model_ps_stamps(sli_model* m, uint64_t* host, int64_t n, int32_t* grid) {
-    SLI_CHECK(m && host && grid, SLI_ERR_ARG, "null argument");
-    SLI_HIP(hipSetDevice(m->c.device));
-    SLI_TRY(ps_setup(m));
-    const int64_t want = (int64_t)(2 + 5 * m->L) * m->ps_grid * 5;
-    *grid = m->ps_grid;
-    SLI_CHECK(n == want, SLI_ERR_SHAPE, "stamp buffer must hold (2 + 5L) * grid * 5 values");
-    struct Guard {
-        void* st = nullptr;
-        void* args = nullptr;
-        ~Guard() {
-            if (st) (void)hipFree(st);
-            if (args) (void)hipFree(args);
-        }
-    } g;
-    SLI_HIP(hipMalloc(&g.st, sizeof(uint64_t) * n));
-    SLI_HIP(hipMalloc(&g.args, sizeof(PsArgs)));
-    PsArgs a;
-    SLI_HIP(hipMemcpy(&a, m->ps_args, sizeof(PsArgs), hipMemcpyDeviceToHost));
-    a.stamps = (unsigned long long*)g.st;
-    SLI_HIP(hipMemcpy(g.args, &a, sizeof(PsArgs), hipMemcpyHostToDevice));
-    SLI_HIP(hipMemsetAsync(g.st, 0, sizeof(uint64_t) * n, m->stream));
-    SLI_HIP(hipMemsetAsync(m->ps_sync, 0, m->ps_sync_bytes, m->stream));
-    a.hd = m->hd;
-    SLI_TRY(ps_launch(a, (const PsArgs*)g.args, m->c.w_dtype, m->c.kv_dtype, m->ps_grid, m->ps_lds, m->stream, false));
-    SLI_HIP(hipStreamSynchronize(m->stream));
-    SLI_HIP(hipMemcpy(host, g.st, sizeof(uint64_t) * n, hipMemcpyDeviceToHost));
     return SLI_OK;
 }
 
@@ -2348,6 +2184,7 @@ int sli_model_time_gemv(sli_model* m, int32_t iters, double* avg_us, double* byt
                         int32_t* launches_per_step) {
     SLI_CHECK(m && iters > 0, SLI_ERR_ARG, "bad argument");
     SLI_HIP(hipSetDevice(m->c.device));
+    SLI_TRY(bg_sync_tiles(m));  // the batched launches stream the fragment-layout copies
     // The probe re-runs the step's weight-streaming launches in place. It saves and restores the residual
     // stream x; its QKV launches rewrite each layer's K/V row at the current position (from the final x),
     // which the next real step at that position overwrites again (the bench's idempotent step does).

@@ -877,14 +877,9 @@ inline int gemv_blocks(int units, int csplit = 1) {
 // gives every wave (nearly) the same count; it is taken when it keeps >= 7/8 of the workgroups, so each
 // CU's share of the HBM stream stays under its per-CU fetch rate (gate/up: 230 workgroups, 31.4 -> 29.0 us,
 // C1 358 -> 368 tok/s; qkv at 1.5 units per wave would need 192 workgroups: measured slower, 17.9 -> 20.5 us;
-// profiles/r3_gemv_balance_ab.txt). SLI_GEMV_BALANCE=0 keeps the full grid (A/B).
+// profiles/r3_gemv_balance_ab.txt).
 inline int gemv_balanced_blocks(int units) {
-    static const bool on = [] {
-        const char* e = getenv("SLI_GEMV_BALANCE");
-        return !(e && e[0] == '0');
-    }();
     const int b = gemv_blocks(units);
-    if (!on) return b;
     const int w = kGemvThreads / 64;
     const int k = (units + b * w - 1) / (b * w);  // most units of a wave at the full grid
     const int g = (units + k * w - 1) / (k * w);
@@ -898,16 +893,11 @@ inline int gemv_balanced_blocks(int units) {
 // half the waves stream for half the launch), ceil(u / k) waves of k units each can take all of them.
 // Measured (profiles/r3_gemv_balance_ab.txt): int8 qkv 12.8 -> 12.4 us with 12 waves of 2 units, C3 +0.8 %;
 // fp16 qkv 18.1 -> 21.2 us (12 waves keep 3/4 of the bytes in flight per CU, and fp16 needs them) — so
-// int8 weights only (the launch sites pass the weight type). SLI_GEMV_WAVES=0 keeps 16 (A/B).
+// int8 weights only (the launch sites pass the weight type).
 template <typename WT>
 inline int gemv_wave_count(int units, int grid) {
     if (!std::is_same<WT, int8_t>::value) return kGemvThreads / 64;
-    static const bool on = [] {
-        const char* e = getenv("SLI_GEMV_WAVES");
-        return !(e && e[0] == '0');
-    }();
     const int w = kGemvThreads / 64;
-    if (!on) return w;
     const int upw = (units + grid - 1) / grid;  // most units of a workgroup
     const int k = (upw + w - 1) / w;
     const int c = (upw + k - 1) / k;

@@ -1,9 +1,11 @@
 // ops.hip — kernel-level C ABI (include/sli.h): one entry point per reference CUDA launcher in
 // include/kernel/cuda/*.cuh, with the reference CPU kernels' semantics (the oracle).
 #include <cmath>
+#include <type_traits>
 #include <vector>
 
 #include "attention.h"
+#include "attn_mfma.h"
 #include "bgemm.h"
 #include "common.h"
 #include "gemv.h"
@@ -160,6 +162,49 @@ int attn_wg_positions(int kv_dtype, int head_dim) {
     return kAttnSlots * (64 / (head_dim / epv));
 }
 
+// The MFMA decode attention (attn_mfma.h) for an fp16 cache. SLI_ATTN_MFMA=0 at build time keeps the
+// register-staged kernel (attention.h) everywhere, for an A/B variant build.
+#ifndef SLI_ATTN_MFMA
+#define SLI_ATTN_MFMA 1
+#endif
+static bool attn_mfma_ok(const AttnArgs<__half>& a, int g) {
+    // the batch-1 MHA step (C1 / C3) merges its splits in the wo GEMV's input staging (defer_merge 1), where the
+    // register-staged kernel's 8.5 us stays ahead (tools/attn_mfma_lab: 9.1 vs 10.6 us at C1, both ramp-bound: 131 KB
+    // per CU); every other fp16 attention (GQA batches and shards, op level) runs on the matrix cores
+    if (!SLI_ATTN_MFMA || a.cache_heads != 0 || !(g == 1 || g == 2 || g == 4 || g == 8) || a.defer_merge == 1)
+        return false;
+    // every 16-byte DMA piece aligned: cache bases, row and head strides, q
+    return (uintptr_t)a.k % 16 == 0 && (uintptr_t)a.v % 16 == 0 && (uintptr_t)a.q % 16 == 0 && a.pos_stride % 8 == 0 &&
+           a.head_stride % 8 == 0;
+}
+template <int HD, int G>
+static void attn_mfma_go(const AttnArgs<__half>& a, int blocks, int nbuf, hipStream_t s) {
+    if (nbuf == 1)
+        hipLaunchKernelGGL((attn_mfma_kernel<HD, G, 1>), dim3(blocks), dim3(64 * kAmWaves), 0, s, a);
+    else
+        hipLaunchKernelGGL((attn_mfma_kernel<HD, G, 2>), dim3(blocks), dim3(64 * kAmWaves), 0, s, a);
+}
+// Split geometry: one workgroup per CU over the whole context (attn_mfma_tpw), its splits merged by the head's
+// last-arriving workgroup inside the launch (a requested merge launch, defer_merge 2, becomes that in-launch
+// merge: the same result in out).
+template <int HD>
+static int attn_mfma_launch(AttnArgs<__half> a, int g, int T, hipStream_t s) {
+    const int tpw = attn_mfma_tpw(a.n_kv_heads, T, device_cus());
+    a.ppwg = kAmWgKeys * tpw;
+    a.max_splits = (T + a.ppwg - 1) / a.ppwg;
+    if (a.max_splits > kAttnMaxWgSplits) return fail(SLI_ERR_SHAPE, "mha: context too long for the split merge");
+    if (a.defer_merge == 2) a.defer_merge = 0;
+    const int blocks = a.n_kv_heads * a.max_splits, nbuf = tpw > 1 ? 2 : 1;
+    switch (g) {
+        case 1: attn_mfma_go<HD, 1>(a, blocks, nbuf, s); break;
+        case 2: attn_mfma_go<HD, 2>(a, blocks, nbuf, s); break;
+        case 4: attn_mfma_go<HD, 4>(a, blocks, nbuf, s); break;
+        default: attn_mfma_go<HD, 8>(a, blocks, nbuf, s); break;
+    }
+    SLI_HIP(hipGetLastError());
+    return SLI_OK;
+}
+
 template <typename KT, int HD>
 static int mha_launch_hd(const float* q, const KT* kc, const KT* vc, float* out, int layer, int pos, const int32_t* pos_dev,
                          int T, int H, int Hkv, long long pos_stride, long long head_stride, long long layer_stride,
@@ -175,26 +220,20 @@ static int mha_launch_hd(const float* q, const KT* kc, const KT* vc, float* out,
     a.cache_heads = cache_heads;
     a.defer_merge = defer_merge;
     int g = H / Hkv;
-    // GQA-4 as two GQA-2 groups per kv head (SLI_ATTN_GQA_SPLIT=2; 4: four MHA heads): the 59-VGPR GQA-2 kernel at 8 waves/SIMD
-    // instead of the 128-VGPR GQA-4 one at 4; the two groups of a kv head are wg_splits blocks apart and read
-    // the same K/V rows. Deferred merges only (partials are indexed by q head; the counters by kv head).
-    // Measured (profiles/r4_gqa_split_ab.txt): Llama-3-8B batch 1 ctx 4096 (8 kv heads x 16 splits = 128
-    // workgroups on 256 CUs) attention 10.7 -> 8.1 us with 2 (287 -> 292 tok/s), 9.2 with 4; C4 (batch 8,
-    // 1024 workgroups) 34.5 -> 41 us with 2, 55 with 4; C4's TP-8 shard (batch 8 x 1 kv head x 16 splits = 128
-    // workgroups, merge launch) 14.5 -> 11.9 us with 2, 12.6 with 4 (profiles/r4_c4_tp_families.txt). Default: 2
-    // where the unsplit grid fills at most half the chip and the merge is deferred, else off.
-    // SLI_ATTN_GQA_SPLIT=1|2|4 forces it.
-    static const int gqa_env = [] {
-        const char* e = getenv("SLI_ATTN_GQA_SPLIT");
-        return e && (e[0] == '1' || e[0] == '2' || e[0] == '4') ? e[0] - '0' : 0;
-    }();
-    const int gqa_split = gqa_env ? gqa_env : (defer_merge != 0 && 2 * Hkv * wg_splits <= device_cus() ? 2 : 1);
-    if (gqa_split > 1 && g == 4 && defer_merge && cache_heads == 0) {
-        g /= gqa_split;
-        a.kv_group = gqa_split;
-        a.n_kv_heads = gqa_split * Hkv;
-        a.seq_heads *= gqa_split;
-        Hkv *= gqa_split;
+    if constexpr (std::is_same<KT, __half>::value) {
+        if (attn_mfma_ok(a, g)) return attn_mfma_launch<HD>(a, g, T, s);
+    }
+    // GQA-4 as two GQA-2 groups per kv head: the 59-VGPR GQA-2 kernel at 8 waves/SIMD instead of the 128-VGPR GQA-4
+    // one at 4; the two groups of a kv head are wg_splits blocks apart and read the same K/V rows. Deferred merges
+    // only (partials are indexed by q head; the counters by kv head), where the unsplit grid fills at most half the
+    // chip. Measured (profiles/r4_gqa_split_ab.txt): Llama-3-8B batch 1 (8 kv heads x 16 splits = 128 workgroups)
+    // attention 10.7 -> 8.1 us; C4 (1024 workgroups) 34.5 -> 41 us, so off there.
+    if (g == 4 && defer_merge && cache_heads == 0 && 2 * Hkv * wg_splits <= device_cus()) {
+        g = 2;
+        a.kv_group = 2;
+        a.n_kv_heads = 2 * Hkv;
+        a.seq_heads *= 2;
+        Hkv *= 2;
     }
     const int blocks = Hkv * wg_splits;
     switch (g) {

@@ -15,13 +15,6 @@ size_t mha_part_bytes(int T, int H, int hd);       // split partials [H][splits]
 size_t mha_workspace_bytes(int T, int H, int hd);  // partials + per-kv-head arrival counters
 int attn_wg_positions(int kv_dtype, int head_dim);  // context positions per attention workgroup
 
-struct PsArgs;
-// persistent batch-1 step (persist.h / persist.hip): positions per attention workgroup -> splits of a
-// context of T positions; launch with the args record a_dev (a copy of a in device memory; prepare = true:
-// only raise the kernel's dynamic-LDS limit)
-int ps_max_splits(int kv_dtype, int hd, int T);
-int ps_launch(const PsArgs& a, const PsArgs* a_dev, int w_dtype, int kv_dtype, int grid, size_t lds, hipStream_t s, bool prepare);
-
 int embedding_launch(int token, const int32_t* token_dev, const void* table, int dtype, const float* row_scale,
                      float* out, int vocab, int dim, hipStream_t s);
 

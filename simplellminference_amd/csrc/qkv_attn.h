@@ -13,7 +13,7 @@
 // drains, and adds its units to its kv heads' counters (one add per workgroup and head, spread over counters on
 // separate lines: attention.h kAttnHandSub); each attention wave waits (bounded) for its
 // kv head's (G + 2) * hd / 2 units, replaces the stale row at pos with the hand-off and reads q by sc1 loads
-// (the hand-off pattern of persist.h, MI355X_MICROARCH.md "Valid forms" row 1). The head's last live attention
+// (MI355X_MICROARCH.md "Valid forms" row 1). The head's last live attention
 // workgroup zeroes the counters, so no memset node is needed between launches.
 //
 // Only the GEMV workgroups are waited on, and they wait on nothing, so the launch drains whatever the
@@ -103,69 +103,12 @@ struct EpiQKVHand : EpiQKV<KT> {
     }
 };
 
-// Chain: the wo GEMV's input stage when wo runs in the same launch, behind the attention (qkv_attn_wo_kernel). Its
-// first weight steps are issued before it waits (kLate: gemv_block issues it after them); wave 0 waits (bounded) for
-// every kv head's merged output (the heads' last attention workgroups count them after their sc1 stores drained),
-// and the threads that hold a float4 of the input read it by sc1 (only those: every workgroup reads the same lines).
-// The last workgroup past the wait zeroes the counters.
-template <int G>
-struct XStageHand {
-    static constexpr bool kLate = true;
-    unsigned* done;   // kv heads merged
-    unsigned* seen;   // wo workgroups past their wait
-    unsigned expect;  // kv heads
-    unsigned nseen;   // wo workgroups
-    int* err;
-    float4 xr[kGemvStageV4];
-    __device__ __forceinline__ void issue(const GemvIn& in) {
-        if (threadIdx.x < 64) {
-            for (unsigned spins = 0; __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < expect;
-                 ++spins) {
-                if (spins >= kAttnHandSpin) {
-                    __hip_atomic_fetch_or(err, kAttnErrHand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
-        }
-        __syncthreads();
-        if (threadIdx.x == 0 &&
-            __hip_atomic_fetch_add(seen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nseen - 1) {
-            __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(seen, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        const int n4 = in.cols >> 2;
-        const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in.x), 0, (unsigned)(in.cols * 4), 0x00020000);
-#pragma unroll
-        for (int k = 0; k < kGemvStageV4; ++k) {
-            const int i = (int)threadIdx.x + k * kGemvThreads;
-            if (i < n4) xr[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16u * i, 0, 16 /* sc1 */));
-        }
-    }
-    __device__ __forceinline__ void commit(float* smem, const GemvIn& in) {
-        float4* xs4 = reinterpret_cast<float4*>(smem + kGemvLdsHead);
-        const int n4 = in.cols >> 2;
-#pragma unroll
-        for (int k = 0; k < kGemvStageV4; ++k) {
-            const int i = (int)threadIdx.x + k * kGemvThreads;
-            if (i < n4) xs4[xswz<G>(i)] = xr[k];
-        }
-    }
-};
-
-// the attention role of the fused launches: split partials, the head's last workgroup merges (and, in a chain,
-// counts the merged head for the wo workgroups)
+// the attention role of the fused launch: split partials, the head's last workgroup merges
 template <typename KT, int HD, int G>
 __device__ __forceinline__ void qkv_attn_role(const AttnArgs<KT>& a) {
     const int kvh = blockIdx.x / a.max_splits;
-    if (attn_publish<KT, HD, G, attn_waves(G), attn_late_v(G), true>(a, kvh, blockIdx.x - kvh * a.max_splits)) {
+    if (attn_publish<KT, HD, G, attn_waves(G), attn_late_v(G), true>(a, kvh, blockIdx.x - kvh * a.max_splits))
         attn_merge<HD, G>(a.part, a.out, kvh, a.max_splits, attn_live_splits<KT, HD, G>(a, kvh), 0, kGemvThreads);
-        if (a.chain_done) {  // every thread's sc1 stores drained (attn_merge): one arrival for the head
-            __syncthreads();
-            if (threadIdx.x == 0)
-                __hip_atomic_fetch_add(a.chain_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
 }
 
 template <typename WT, int U, typename KT, int HD, int G>
@@ -182,30 +125,6 @@ __global__ void __launch_bounds__(kGemvThreads) qkv_attn_kernel(const WT* __rest
     gemv_block<WT, 2, U, true, EpiQKVHand<KT>, XStage<Vec16<WT>::N / 4>, 2, true, true>(W, in, epi, stage, smem);
 }
 
-// The chain: attention [0, n_attn), q/k/v GEMV [n_attn, wo.blk0), then the wo GEMV [wo.blk0, grid). The wo workgroups
-// are dispatched as the q/k/v workgroups retire, stream their first weight steps while the attention finishes, and
-// wait for the merged heads (XStageHand). Every wait is on lower-indexed workgroups, which never wait on higher ones.
-template <typename WT, int U, typename KT, int HD, int G, class WoEpi, int UO>
-__global__ void __launch_bounds__(kGemvThreads)
-    qkv_attn_wo_kernel(const WT* __restrict__ W, GemvIn in, EpiQKVHand<KT> epi_in, AttnArgs<KT> a,
-                       const WT* __restrict__ Wo, GemvIn in_wo, WoEpi wo_epi_in, XStageHand<Vec16<WT>::N / 4> wo_stage) {
-    static_assert(attn_waves(G) * 64 == kGemvThreads, "the attention workgroups must be GEMV-sized (G <= 2)");
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    if ((int)blockIdx.x < in.blk0) {
-        qkv_attn_role<KT, HD, G>(a);
-        return;
-    }
-    if ((int)blockIdx.x < in_wo.blk0) {
-        EpiQKVHand<KT> epi = epi_in;  // (in.blk1 = in_wo.blk0: the q/k/v partition ends where wo's workgroups begin)
-        XStage<Vec16<WT>::N / 4> stage;
-        gemv_block<WT, 2, U, true, EpiQKVHand<KT>, XStage<Vec16<WT>::N / 4>, 2, true, true>(W, in, epi, stage, smem);
-        return;
-    }
-    WoEpi epi = wo_epi_in;
-    XStageHand<Vec16<WT>::N / 4> stage = wo_stage;
-    gemv_block<WT, 1, UO, true, WoEpi, XStageHand<Vec16<WT>::N / 4>, 2, false, true>(Wo, in_wo, epi, stage, smem);
-}
-
 // Launch, or hipErrorNotSupported when the shape does not qualify (the caller then runs the two launches):
 // G <= 2, hd 64 / 128, and an attention grid of at most a quarter of the persistent GEMV grid (TP shards and
 // small models; every TP-1 preset's is larger). a: the attention's arguments as mha_launch builds them, hand_* filled in.
@@ -217,12 +136,9 @@ hipError_t launch_qkv_attn(const WT* W, const GemvIn& in_, const EpiQKVHand<KT>&
     const int g = e.g;
     const int n_attn = a.n_kv_heads * a.max_splits;
     const int maxb = gemv_max_blocks();
-    // the attention's share of the grid: at most 1 / qa_div of the CUs (SLI_QKV_ATTN_DIV, default 4; A/B knob)
-    static const int qa_div = [] {
-        const char* e = getenv("SLI_QKV_ATTN_DIV");
-        return e && atoi(e) >= 2 ? atoi(e) : 4;
-    }();
-    if ((g != 1 && g != 2) || (hd != 64 && hd != 128) || qa_div * n_attn > maxb || a.n_kv_heads > kGemvLdsHead)
+    // the attention's share of the grid: at most a quarter of the CUs (half measured slower at TP 2: the q/k/v
+    // GEMV's grid shrinks more than the attention gains, profiles/r4_qkv_attn_tp.txt)
+    if ((g != 1 && g != 2) || (hd != 64 && hd != 128) || 4 * n_attn > maxb || a.n_kv_heads > kGemvLdsHead)
         return hipErrorNotSupported;
     const GemvSplit sp = gemv_split<WT, 4>(units, in_.cols);  // (CS 1 runs the split instantiation unsplit)
     if (dry) return hipSuccess;  // (sli_model_fused_qkv_attn: would launch)
@@ -258,71 +174,6 @@ hipError_t launch_qkv_attn(const WT* W, const GemvIn& in_, const EpiQKVHand<KT>&
 #undef SLI_QA_HD
 #undef SLI_QA_G
 #undef SLI_QA
-    return hipGetLastError();
-}
-
-// The chain launch (q/k/v + attention + wo), fp16 weights: hipErrorNotSupported where launch_qkv_attn would refuse,
-// where wo's GEMV would be column-split, or where the grid outgrows the per-workgroup exchange's flag slots.
-// a.defer_merge must be 0 (the heads' last workgroups merge) and a.chain_done set; done / seen: two counters on
-// separate lines, zero between launches.
-template <typename KT, class WoEpi>
-hipError_t launch_qkv_attn_wo(const __half* W, const GemvIn& in_, const EpiQKVHand<KT>& e, const AttnArgs<KT>& a,
-                              int units, int hd, const __half* Wo, const GemvIn& in_wo_, const WoEpi& wo_epi,
-                              int wo_units, unsigned* done, unsigned* seen, int max_grid, hipStream_t s,
-                              bool dry = false) {
-    const int g = e.g;
-    const int n_attn = a.n_kv_heads * a.max_splits;
-    const int maxb = gemv_max_blocks();
-    if ((g != 1 && g != 2) || (hd != 64 && hd != 128) || 4 * n_attn > maxb || a.n_kv_heads > kGemvLdsHead ||
-        a.defer_merge != 0 || !a.chain_done)
-        return hipErrorNotSupported;
-    const GemvSplit sp = gemv_split<__half, 4>(units, in_.cols);
-    if (gemv_split<__half, 2>(wo_units, in_wo_.cols).cs != 1) return hipErrorNotSupported;
-    const int grid_g = std::min(gemv_blocks(units, sp.cs), maxb - n_attn);
-    const int grid_o = gemv_balanced_blocks(wo_units);
-    if (n_attn + grid_g + grid_o > max_grid) return hipErrorNotSupported;
-    if (dry) return hipSuccess;
-    GemvIn in = in_;
-    in.csplit = sp.cs;
-    in.cw = kGemvThreads / 64;
-    in.blk0 = n_attn;
-    in.blk1 = n_attn + grid_g;
-    GemvIn in_wo = in_wo_;
-    in_wo.csplit = 1;
-    in_wo.cw = gemv_wave_count<__half>(wo_units, grid_o);
-    in_wo.blk0 = n_attn + grid_g;
-    const XStageHand<2> st{done, seen, (unsigned)a.n_kv_heads, (unsigned)grid_o, a.hand_err};
-    const size_t lds =
-        std::max(gemv_lds_bytes(in.cols) + sizeof(float) * gemv_res_floats(units, grid_g, 2, sp.cs),
-                 gemv_lds_bytes(in_wo.cols) + sizeof(float) * gemv_res_floats(wo_units, grid_o, 1));
-    const dim3 grid(n_attn + grid_g + grid_o), blk(kGemvThreads);
-#define SLI_QAW(U_, HD_, G_)                                                                                         \
-    hipLaunchKernelGGL((qkv_attn_wo_kernel<__half, U_, KT, HD_, G_, WoEpi, 2>), grid, blk, lds, s, W, in, e, a, Wo, \
-                       in_wo, wo_epi, st)
-#define SLI_QAW_G(U_, HD_) \
-    do {                   \
-        if (g == 1)        \
-            SLI_QAW(U_, HD_, 1); \
-        else               \
-            SLI_QAW(U_, HD_, 2); \
-    } while (0)
-#define SLI_QAW_HD(U_) \
-    do {               \
-        if (hd == 128) \
-            SLI_QAW_G(U_, 128); \
-        else           \
-            SLI_QAW_G(U_, 64); \
-    } while (0)
-    if (sp.u == 4) {
-        SLI_QAW_HD(4);
-    } else if (sp.u == 2) {
-        SLI_QAW_HD(2);
-    } else {
-        SLI_QAW_HD(1);
-    }
-#undef SLI_QAW_HD
-#undef SLI_QAW_G
-#undef SLI_QAW
     return hipGetLastError();
 }
 

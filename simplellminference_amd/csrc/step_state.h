@@ -11,7 +11,7 @@ struct DevState {
     int32_t n_forced;     // prompt length (teacher forcing while pos < n_forced)
     int32_t last_argmax;  // greedy argmax of the last step's logits
     int32_t advance;      // 1: finalize advances pos/token; 0: idempotent step (bench)
-    int32_t error;        // device-side error bits: kPsErrTimeout (persist.h), kOsErrTimeout (oneshot.h);
+    int32_t error;        // device-side error bits: kOsErrTimeout (oneshot.h), kAttnErrHand (attention.h);
                           // checked by every predict path
     unsigned long long key;  // argmax key of the last step (0 between steps)
 };

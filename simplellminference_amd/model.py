@@ -159,10 +159,10 @@ class LlamaModel:
         return max(0, min(chunk, c.vocab_size - self.tp_rank * chunk))
 
     # ------------------------------------------------------------------ execution
-    EXEC = {"launches": 0, "persistent": 1}
+    EXEC = {"launches": 0}
 
     def set_exec(self, mode: str) -> "LlamaModel":
-        """"launches" (one graph of fused launches) or "persistent" (the whole step as one launch)."""
+        """"launches": one graph of fused launches (the only mode since round 5)."""
         call("sli_model_set_exec", self._h, self.EXEC[mode])
         return self
 
@@ -240,8 +240,8 @@ class LlamaModel:
         return "mfma" if _lib.load().sli_model_prefill_path(self._h) == 1 else "decode"
 
     def fused_qkv_attn(self) -> int:
-        """1 when the decode step runs q/k/v + attention as one launch per layer, 2 when wo joins it too (the chain),
-        0 otherwise: sli_model_fused_qkv_attn."""
+        """1 when the decode step runs q/k/v + attention as one launch per layer, 0 otherwise:
+        sli_model_fused_qkv_attn."""
         return int(_lib.load().sli_model_fused_qkv_attn(self._h))
 
     def predict_prefill(self, prompt_ids, max_length: int, want_logits: bool = False):

@@ -147,15 +147,14 @@ def test_short_context_many_heads(gpu, oracle):
 
 
 @pytest.mark.parametrize("name,fixture", [("tiny", "c0_mha.npz"), ("tiny-gqa", "c0_gqa.npz")])
-@pytest.mark.parametrize("exec_mode", ["launches", "persistent"])
-def test_tiny_predict_matches_committed_golden(gpu, name, fixture, exec_mode):
+def test_tiny_predict_matches_committed_golden(gpu, name, fixture):
     """Config C0 (fp32 weights and KV) against the COMMITTED fixtures (tests/golden/*.npz), not a live
     oracle run: a silent oracle regression cannot move both sides together here. Tokens bit-exact,
     logits within 1e-4."""
     import os
     from simplellminference_amd.model import LlamaModel, preset
     g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", fixture))
-    gm = LlamaModel(config=preset(name), w_dtype="f32", kv_dtype="f32", seed=0).init().set_exec(exec_mode)
+    gm = LlamaModel(config=preset(name), w_dtype="f32", kv_dtype="f32", seed=0).init()
     toks, logits = gm.predict([int(t) for t in g["prompt"]], 36, want_logits=True)
     gm.close()
     assert np.array_equal(toks, g["tokens"]), (toks, g["tokens"])

@@ -155,17 +155,6 @@ def test_prefill_f32_weights_teacher_forces(gpu, oracle):
     _check(gtok, glog, otok, olog, 13, tol=1e-4)
 
 
-def test_prefill_then_persistent_decode(gpu, oracle):
-    cfg, om, gm = _pair(oracle, "tiny")
-    gm.set_exec("persistent")
-    prompt = _prompt(19, cfg.vocab_size)
-    otok, _ = om.predict(prompt, 36)
-    gtok = gm.predict_prefill(prompt, 36)
-    gm.close()
-    om.close()
-    assert np.array_equal(gtok, otok)
-
-
 def test_prefill_twice_reuses_graphs(gpu, oracle):
     """A second prompt on the same model (graphs already captured, other chunk sizes) gives the oracle's
     tokens too: the chunk position and count come from device memory, not from the capture."""

@@ -150,8 +150,6 @@ def _oneshot_rank(rank, world, port, name, batch, q, mode="oneshot", w="f16", pr
     mode, _, qa = mode.partition("+")  # "+qa": q/k/v + attention as one launch (qkv_attn.h) on the ranks too
     if qa:
         os.environ["SLI_QKV_ATTN"] = "1"
-    if qa == "qac":  # and wo in the same launch (the chain)
-        os.environ["SLI_QKV_CHAIN"] = "1"
     if mode == "fused_wg":  # every workgroup waits for its peers': the ranks' grids must fit the one GPU together
         os.environ["SLI_DEBUG_GEMV_MAX_BLOCKS"] = str(256 // (2 * world))
     import torch
@@ -192,8 +190,8 @@ def _oneshot_rank(rank, world, port, name, batch, q, mode="oneshot", w="f16", pr
                                              ("tiny-h8", 1, "fused_wg"), ("tiny-gqa", 2, "fused_wg"),
                                              ("llama3-8b:2", 8, "fused_wg"), ("llama3-8b:2", 8, "oneshot"),
                                              ("tiny", 1, "fused_wg+qa"), ("tiny-gqa", 1, "oneshot+qa"),
-                                             ("tiny", 1, "fused_wg+qac"), ("tiny-gqa", 1, "oneshot+qac")])
-def test_oneshot_allreduce_two_processes(gpu, name, batch, mode):
+                                             ("tiny-gqa", 1, "fused+qa")])
+def test_oneshot_allreduce_two_processes(gpu, oracle, name, batch, mode):
     """The one-shot all-reduce (oneshot.h) between two rank PROCESSES through IPC-mapped uncached buffers
     (both on device 0 here; on the 8-GPU node each on its own GPU, over xGMI): greedy tokens identical to
     the TP = 1 engine, logits within 1e-3, no device error (the bounded waits never gave up). mode "fused":
@@ -222,6 +220,10 @@ def test_oneshot_allreduce_two_processes(gpu, name, batch, mode):
     assert err == 0
     assert np.array_equal(toks, rtoks)
     assert np.abs(logits - rlogits).max() <= 1e-3
+    if mode.endswith("+qa"):
+        otoks, ologits = _oracle_for(oracle, name, oracle.W_F16, True).predict(PROMPT, 16)
+        assert np.array_equal(toks, otoks)
+        assert np.abs(logits - ologits).max() <= 1e-3
 
 
 @pytest.mark.parametrize("mode", ["oneshot", "fused"])
@@ -258,8 +260,8 @@ def test_oneshot_prefill_two_processes(gpu, mode):
                                                ("tiny-gqa", 2, "fused", "i8"), ("tiny-h8", 4, "fused_wg", "f16"),
                                                ("tiny-gqa", 2, "fused_wg", "i8"), ("llama2-7b:2", 2, "fused_wg", "f16"),
                                                ("llama2-7b:2", 2, "fused", "f16"), ("tiny-h8", 4, "fused_wg+qa", "f16"),
-                                               ("tiny-gqa", 2, "fused+qa", "i8"), ("tiny-h8", 4, "fused_wg+qac", "f16")])
-def test_oneshot_allreduce_more_ranks(gpu, name, world, mode, w):
+                                               ("tiny-gqa", 2, "fused+qa", "i8"), ("tiny-h8", 4, "fused+qa", "f16")])
+def test_oneshot_allreduce_more_ranks(gpu, oracle, name, world, mode, w):
     """The one-shot exchange (separate launch or fused into wo / down) between 4 rank processes on one GPU, the
     fused forms with int8 weights, and both fused forms at Llama-2-7B shard shapes (2 layers, TP 2: 64 / 256
     workgroups per wo / down launch): tokens identical to the TP = 1 engine, logits within 1e-3, no device
@@ -281,3 +283,7 @@ def test_oneshot_allreduce_more_ranks(gpu, name, world, mode, w):
     assert err == 0
     assert np.array_equal(toks, rtoks)
     assert np.abs(logits - rlogits).max() <= 1e-3
+    if mode.endswith("+qa"):
+        otoks, ologits = _oracle_for(oracle, name, oracle.W_F16 if w == "f16" else oracle.W_I8, True).predict(PROMPT, 16)
+        assert np.array_equal(toks, otoks)
+        assert np.abs(logits - ologits).max() <= 1e-3

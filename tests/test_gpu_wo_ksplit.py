@@ -72,7 +72,7 @@ def test_ctx4096_sixteen_splits_wo_ksplit(gpu, oracle, monkeypatch, merge, ks):
 
 @pytest.mark.parametrize("ks", ["2", "4"])
 def test_wo_ksplit_greedy_and_prefill(gpu, oracle, monkeypatch, ks):
-    """Prefill (chunked MFMA GEMMs, not split) then K-split decode steps; the persistent step alongside."""
+    """Prefill (chunked MFMA GEMMs, not split) then K-split decode steps."""
     monkeypatch.setenv("SLI_WO_KSPLIT", ks)
     om, gm = _models(oracle, "tiny-gqa", "f16", "f16", max_length=160)
     prompt = [int(t) for t in np.random.default_rng(5).integers(0, 512, 70)]

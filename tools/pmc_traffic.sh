@@ -10,6 +10,6 @@ timeout -s KILL 420 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc -o fetch --outp
 csvf=$(find gpurun_out/pmc -name 'fetch_counter_collection.csv' | head -1)  # rocprofv3 may or may not add a subdirectory
 [ -n "$csvf" ] || { echo "PMC: no counter csv"; exit 1; }
 read alg dom < <(grep '^{' gpurun_out/pmc/bench.log | tail -1 | python3 -c "import json,sys; r=json.loads(sys.stdin.read())['roofline']; print(r['algorithmic_bytes_per_launch'], r['kernel'].split(':')[0])")
-python3 tools/pmc_traffic.py "$csvf" "$alg" "gpurun_out/pmc/${tag}_gemv_traffic.json" "${KEY:-llama2-7b/f16/tp1}" "$dom" || exit 1
+python3 tools/pmc_traffic.py "$csvf" "$alg" "gpurun_out/pmc/${tag}_gemv_traffic.json" "${KEY:-llama2-7b/f16/tp1}" "$dom" gpurun_out/pmc/bench.log || exit 1
 mv "$csvf" "gpurun_out/pmc/${tag}_${KEY//\//_}_fetch_counter_collection.csv"
 rm -rf gpurun_out/pmc/*/ gpurun_out/pmc/fetch_*.csv  # the raw per-run files: the next pass must not find them

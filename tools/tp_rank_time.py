@@ -1,7 +1,7 @@
 """Per-rank decode-step time of one tensor-parallel shard on ONE GPU, without a communicator
 (SLI_DEBUG_NOCOMM: the rank's kernels at their real shapes, no RCCL all-reduces; values are not a model).
 Estimates the compute part of config C2 (Llama-2-7B at TP N); the collectives come on top.
-    python tools/tp_rank_time.py [N ...]            (TP_EXEC=persistent: the one-launch step instead)
+    python tools/tp_rank_time.py [N ...]
 TP_AR=oneshot|fused: the rank's all-reduces included, in loopback (SLI_DEBUG_OS_LOOPBACK: the exchange kernels
 run against the rank's own comm buffer, every flag raised locally — everything but the xGMI hop).
 """
@@ -24,11 +24,6 @@ for world in [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]:
     m = LlamaModel(config=preset(PRESET, max_length=CTX), w_dtype="f16", kv_dtype="f16", seed=1, tp_rank=world - 1,
                    tp_size=world, batch=BATCH).init()
     m.fill_kv_synthetic(7, CTX - 1)
-    if os.environ.get("TP_EXEC"):
-        try:
-            m.set_exec(os.environ["TP_EXEC"])
-        except Exception as e:  # noqa: BLE001 - report and go on with the launch graph
-            print(f"tp{world}: {os.environ['TP_EXEC']} refused ({e})", flush=True)
     ar = os.environ.get("TP_AR")
     if ar and world > 1:
         os.environ["SLI_DEBUG_OS_LOOPBACK"] = "1"
