@@ -92,6 +92,7 @@ __device__ __forceinline__ uint2 am_tr_read(unsigned lds_addr) {
     return v;
 }
 typedef _Float16 am_half8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef float am_float4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ am_float4 am_mfma(const u32x4& a, const u32x4& b, am_float4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(am_half8, a), __builtin_bit_cast(am_half8, b), c,
@@ -108,60 +109,68 @@ __device__ __forceinline__ void am_split3(float v, __half& hi, __half& mid, __ha
     lo = __float2half_rn(r - __half2float(mid));
 }
 
-// The head's last-arriving workgroup merges its ns live split partials into out, in split order whatever the
-// arrival order (M = max m_i, w_i = e^{m_i - M}, out = sum w_i o_i / sum w_i l_i, attention.h attn_merge): every
-// thread owns OUT outputs (q head g, dim d) and issues the loads of all of them for a batch of NS splits together
-// (write-through copies, sc1), so up to NS splits cost ONE round trip; past NS the batches merge online (the
-// running sums rescaled to each batch's new max). Up to NS splits the sums are attn_merge's, bit for bit.
-template <int HD, int G, int NS>
+// The head's last-arriving workgroup merges its ns live split partials into out (attention.h attn_merge's
+// arithmetic: M = max m_i, w_i = e^{m_i - M}, out = sum w_i o_i / sum w_i l_i). A thread pair owns 4 consecutive
+// outputs (q head g, dims d .. d+3): each thread of the pair merges every other split (its own max, rescaled
+// sums), loading all of them in ONE batch of 16-byte o and 8-byte (m, l) write-through copies (sc1; 16 splits
+// per thread: ns <= 32 in one round trip), and the pair combines over DPP (lanes 2j, 2j+1). Deterministic: a
+// fixed split-to-thread map and combine order.
+template <int HD, int G, int NSH>
 __device__ __forceinline__ void am_merge(const float* part, float* out, int kvh, int max_splits, int ns) {
-    constexpr int PS = HD + kAttnPartPad, NO = G * HD, NTH = 64 * kAmWaves, OUT = (NO + NTH - 1) / NTH;
+    constexpr int PS = HD + kAttnPartPad, NOG = G * HD / 4, NTH = 64 * kAmWaves, NPASS = (2 * NOG + NTH - 1) / NTH;
     const unsigned bytes = (unsigned)(sizeof(float) * (size_t)G * max_splits * PS);
-    const float* base = part + (size_t)kvh * G * max_splits * PS;
-    float M[OUT], o[OUT], L[OUT];
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(part + (size_t)kvh * G * max_splits * PS), 0,
+                                                      bytes, 0x00020000);
+    const int half = threadIdx.x & 1;
 #pragma unroll
-    for (int u = 0; u < OUT; ++u) {
-        M[u] = -INFINITY;
-        o[u] = 0.0f;
-        L[u] = 0.0f;
-    }
-    for (int s0 = 0; s0 < ns; s0 += NS) {
-        float mv[OUT][NS], lv[OUT][NS], ov[OUT][NS];
+    for (int pass = 0; pass < NPASS; ++pass) {
+        const int og = min((int)(threadIdx.x >> 1) + pass * (NTH / 2), NOG - 1);  // (clamped: every lane of the pair
+        const int g = og / (HD / 4), d = (og % (HD / 4)) * 4;                  //  computes, only valid ones store)
+        float M = -INFINITY, L = 0.0f;
+        float4 o = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        for (int s0 = half; s0 < ns; s0 += 2 * NSH) {
+            u32x4 ov[NSH];
+            u32x2 ml[NSH];
 #pragma unroll
-        for (int u = 0; u < OUT; ++u) {
-            const int i = min((int)threadIdx.x + u * NTH, NO - 1);
-            const int g = i / HD, d = i - g * HD;
-#pragma unroll
-            for (int j = 0; j < NS; ++j) {
-                const unsigned r = (unsigned)(g * max_splits + min(s0 + j, ns - 1)) * PS;
-                mv[u][j] = load_sc1(base, bytes, 4u * (r + HD));
-                lv[u][j] = load_sc1(base, bytes, 4u * (r + HD + 1));
-                ov[u][j] = load_sc1(base, bytes, 4u * (r + d));
+            for (int j = 0; j < NSH; ++j) {  // splits s0, s0 + 2, ... (clamped to the last live split of this half)
+                const int sj = min(s0 + 2 * j, ns - 1 - ((ns - 1 - half) & 1));
+                const unsigned r = (unsigned)(g * max_splits + sj) * PS;
+                ov[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, 4u * (r + d), 0, 16 /* sc1 */);
+                ml[j] = __builtin_amdgcn_raw_buffer_load_b64(rs, 4u * (r + HD), 0, 16);
             }
-        }
+            float mb = M;
 #pragma unroll
-        for (int u = 0; u < OUT; ++u) {
-            float mb = M[u];
+            for (int j = 0; j < NSH; ++j) mb = fmaxf(mb, __uint_as_float(ml[j].x));  // duplicates leave the max
+            const float c = expf(M - mb);  // 0 on the first batch
+            o.x *= c, o.y *= c, o.z *= c, o.w *= c;
+            L *= c;
 #pragma unroll
-            for (int j = 0; j < NS; ++j) mb = fmaxf(mb, mv[u][j]);  // clamped duplicates leave the max
-            const float c = expf(M[u] - mb);  // 0 on the first batch
-            o[u] *= c;
-            L[u] *= c;
-#pragma unroll
-            for (int j = 0; j < NS; ++j) {
-                if (s0 + j < ns) {
-                    const float w = expf(mv[u][j] - mb);
-                    o[u] = fmaf(w, ov[u][j], o[u]);
-                    L[u] = fmaf(w, lv[u][j], L[u]);
+            for (int j = 0; j < NSH; ++j) {
+                if (s0 + 2 * j < ns) {
+                    const float w = expf(__uint_as_float(ml[j].x) - mb);
+                    o.x = fmaf(w, __uint_as_float(ov[j].x), o.x);
+                    o.y = fmaf(w, __uint_as_float(ov[j].y), o.y);
+                    o.z = fmaf(w, __uint_as_float(ov[j].z), o.z);
+                    o.w = fmaf(w, __uint_as_float(ov[j].w), o.w);
+                    L = fmaf(w, __uint_as_float(ml[j].y), L);
                 }
             }
-            M[u] = mb;
+            M = mb;
         }
-    }
-#pragma unroll
-    for (int u = 0; u < OUT; ++u) {
-        const int i = (int)threadIdx.x + u * NTH;
-        if (i < NO) out[(size_t)kvh * NO + i] = o[u] / L[u];
+        // the pair: the even lane's splits first (a fixed order)
+        const float Mp = dpp_f<kDppXor1>(M), Lp = dpp_f<kDppXor1>(L);
+        const float4 op = make_float4(dpp_f<kDppXor1>(o.x), dpp_f<kDppXor1>(o.y), dpp_f<kDppXor1>(o.z),
+                                      dpp_f<kDppXor1>(o.w));
+        const float Mt = fmaxf(M, Mp);  // finite: split 0 is live, and it is the even lane's
+        const float ce = expf((half ? Mp : M) - Mt), co = expf((half ? M : Mp) - Mt);  // even, odd lane's weights
+        const float4 oe = half ? op : o, oo = half ? o : op;
+        const float Le = half ? Lp : L, Lo = half ? L : Lp;
+        const float Lt = fmaf(ce, Le, co * Lo);
+        const int ogv = (int)(threadIdx.x >> 1) + pass * (NTH / 2);
+        if (half == 0 && ogv < NOG)
+            *reinterpret_cast<float4*>(out + (size_t)kvh * G * HD + (size_t)g * HD + d) =
+                make_float4(fmaf(ce, oe.x, co * oo.x) / Lt, fmaf(ce, oe.y, co * oo.y) / Lt,
+                            fmaf(ce, oe.z, co * oo.z) / Lt, fmaf(ce, oe.w, co * oo.w) / Lt);
     }
 }
 
@@ -380,19 +389,18 @@ __global__ void __launch_bounds__(64 * kAmWaves) attn_mfma_kernel(AttnArgs<__hal
             acc += *reinterpret_cast<const am_float4*>(reinterpret_cast<const float*>(sm + w * WB) + (t * 64 + lane) * 4) *
                    w4[w];
         if (i16 < G) {  // lane holds d = 16 t + 4 g + r of q head kvh * G + i16
-            float* dst = a.part + ((size_t)(kvh * G + i16) * a.max_splits + wgs) * (HD + kAttnPartPad);
-            if (publish) {  // write-through for the head's last-arriving workgroup (attention.h attn_publish)
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    __hip_atomic_store(dst + t * 16 + 4 * g + r, acc[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const size_t row = ((size_t)(kvh * G + i16) * a.max_splits + wgs) * (HD + kAttnPartPad);
+            if (publish) {  // write-through (sc1, 16- and 8-byte stores) for the head's last-arriving workgroup
+                const auto rs = __builtin_amdgcn_make_buffer_rsrc(a.part + row, 0, 4u * (HD + kAttnPartPad), 0x00020000);
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    u32x4{__float_as_uint(acc[0]), __float_as_uint(acc[1]), __float_as_uint(acc[2]), __float_as_uint(acc[3])},
+                    rs, 4u * (t * 16 + 4 * g), 0, 16 /* sc1 */);
+                if (t == 0 && g == 0)
+                    __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(M), __float_as_uint(L)}, rs, 4u * HD, 0, 16);
             } else {
+                float* dst = a.part + row;
                 *reinterpret_cast<float4*>(dst + t * 16 + 4 * g) = float4{acc[0], acc[1], acc[2], acc[3]};
-            }
-            if (t == 0 && g == 0) {
-                if (publish) {
-                    __hip_atomic_store(dst + HD, M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(dst + HD + 1, L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                } else {
+                if (t == 0 && g == 0) {
                     dst[HD] = M;
                     dst[HD + 1] = L;
                 }
@@ -411,8 +419,10 @@ __global__ void __launch_bounds__(64 * kAmWaves) attn_mfma_kernel(AttnArgs<__hal
     __syncthreads();
     if (last) {
         if (ns <= 4)
-            am_merge<HD, G, 4>(a.part, a.out, kvh, a.max_splits, ns);
+            am_merge<HD, G, 2>(a.part, a.out, kvh, a.max_splits, ns);
         else if (ns <= 8)
+            am_merge<HD, G, 4>(a.part, a.out, kvh, a.max_splits, ns);
+        else if (ns <= 16)
             am_merge<HD, G, 8>(a.part, a.out, kvh, a.max_splits, ns);
         else
             am_merge<HD, G, 16>(a.part, a.out, kvh, a.max_splits, ns);
