@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Float64 restatement of the C4 decode step across the short-context band, as a fixture.
 
-    python tests/golden/make_f64_c4_band.py      # ~30-60 min on 8 cores, ~20 GB of host memory
+    python tests/golden/make_f64_c4_band.py      # ~5 min on 8 cores, ~20 GB of host memory
 
 make_f64_c4.py showed that at a context of two positions every fp32 path (the oracle's sequential sums, six
 BLAS / column-block orders, the GPU) lands 1.0-1.4e-3 from float64 on Llama-3-8B: 32 layers amplify which side
@@ -11,8 +11,9 @@ whole band of short contexts, positions 1..8, one step per position: sequence b 
 at position b + 1. Per position it stores the float64 logits, the oracle's (fp32 sequential, the reference's own
 CPU order) distance to them, and the distances of six more fp32 restatements that differ only in their
 dot-product summation order (BLAS over the whole row, or the row cut into c column blocks summed in block
-order, c = 2..64). test_gpu_batch.py holds the GPU to 1.1x the worst fp32 distance at each position, argmax
-equal. Weights: the synthetic generator's Llama-3-8B (oracle.synth_fill, fp16-rounded as the device holds them;
+order, c = 2..64), and those orders' distances to the oracle itself: where even they exceed 1e-3, no fp32
+implementation can promise the north star's 1e-3 against the reference there. test_gpu_batch.py holds the GPU to
+1.1x the worst fp32 distance to float64 at each position, argmax equal. Weights: the synthetic generator's Llama-3-8B (oracle.synth_fill, fp16-rounded as the device holds them;
 norms fp32); the reference's fp32 RoPE table; model.cpp:40-140 op order; the new K/V row rounded to fp16 as the
 cache stores it (mha_kernel.cpp:36-77 softmax; swiglu_kernel.cpp:12-13 sigmoid(g) * u)."""
 import os
@@ -125,19 +126,23 @@ def main():
     logits = (emb @ rms(X["f64"], wl, np.float64)).T  # [NB][V]
     emb32 = emb.astype(np.float32)
     spread = np.zeros((NB, len(PATHS) - 1))
+    vs_oracle = np.zeros((NB, len(PATHS) - 1))  # each fp32 order against the oracle (the reference's own order)
     for i, (n, dt, c) in enumerate(PATHS[1:]):
         lg = mm(emb32, rms(X[n], wl.astype(np.float32), np.float32), np.float32, c).T
         spread[:, i] = np.abs(lg - logits).max(axis=1)
+        vs_oracle[:, i] = [float(np.abs(lg[b] - want32[b]).max()) for b in range(NB)]
     oracle_err = np.array([float(np.abs(want32[b] - logits[b]).max()) for b in range(NB)])
     for b in range(NB):
-        print(f"pos {POSITIONS[b]}: oracle vs float64 {oracle_err[b]:.3e}; fp32 orders {np.array2string(spread[b], precision=3)}; "
+        fmt = {"float_kind": lambda v: f"{v:.2e}"}
+        print(f"pos {POSITIONS[b]}: oracle vs float64 {oracle_err[b]:.3e}; fp32 orders vs float64 "
+              f"{np.array2string(spread[b], formatter=fmt)} vs the oracle {np.array2string(vs_oracle[b], formatter=fmt)}; "
               f"|logit|max {np.abs(logits[b]).max():.3f}; argmax {int(np.argmax(want32[b]))} vs {int(np.argmax(logits[b]))}",
               flush=True)
     # float32 copy of the float64 logits (6e-8 relative: far inside the 1e-3 bar it serves)
     np.savez_compressed(os.path.join(HERE, "c4_f64_band.npz"), logits=logits.astype(np.float32),
                         tokens=np.array(TOKENS, np.int32), positions=np.array(POSITIONS, np.int32),
                         kv_seeds=np.array(KV_SEEDS, np.int32), seed=np.int32(SEED), oracle_err=oracle_err,
-                        fp32_spread=spread, fp32_paths=np.array([n for n, _, _ in PATHS[1:]]),
+                        fp32_spread=spread, fp32_vs_oracle=vs_oracle, fp32_paths=np.array([n for n, _, _ in PATHS[1:]]),
                         argmax=np.argmax(logits, axis=1).astype(np.int32),
                         oracle_argmax=np.array([int(np.argmax(w)) for w in want32], np.int32))
 

@@ -193,6 +193,36 @@ def test_llama3_8b_full_batch8_matches_oracle(gpu, oracle):
     assert all(e <= b for e, b in zip(errs, bound)), errs
 
 
+@pytest.mark.timeout(600)
+def test_llama3_8b_short_context_band_vs_float64(gpu):
+    """The C4 model (Llama-3-8B, 32 layers, batch 8) at the short contexts where 32 layers amplify the fp16 rounding
+    of every layer's new K/V row: sequence b at position b + 1 (b = 0..7), against the float64 restatement of the
+    same eight steps (tests/golden/make_f64_c4_band.py -> c4_f64_band.npz). At each position the bar is the fp32
+    conditioning measured there: GPU vs float64 within 1.1x the largest float64 distance of seven fp32 paths (the
+    oracle's sequential sums, BLAS, and five column-block orders), argmax equal. The fixture's distances of those
+    orders to the oracle itself (fp32_vs_oracle) show where the north star's 1e-3 against the reference cannot hold
+    for ANY fp32 order; past position 8 the full test below holds every sequence to 1e-3 absolute
+    against the oracle."""
+    import os
+    from simplellminference_amd.model import LlamaModel, preset
+    f64 = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c4_f64_band.npz"))
+    tokens, positions = [int(t) for t in f64["tokens"]], [int(p) for p in f64["positions"]]
+    assert [int(s) for s in f64["kv_seeds"]] == [7 + b for b in range(8)] and positions == list(range(1, 9))
+    gm = LlamaModel(config=preset("llama3-8b"), w_dtype="f16", kv_dtype="f16", seed=1, batch=8).init()
+    gm.fill_kv_synthetic(7, 9)  # sequence b: seed 7 + b, rows 0..8
+    got = gm.forward_batch(tokens, positions)
+    gm.close()
+    rows = []
+    for b in range(8):
+        err = float(np.abs(got[b] - f64["logits"][b]).max())
+        worst = max(float(f64["oracle_err"][b]), float(np.max(f64["fp32_spread"][b])))
+        rows.append((positions[b], err, worst))
+        assert int(np.argmax(got[b])) == int(f64["argmax"][b]), b
+    print("C4 band (pos, GPU vs float64, worst fp32 order vs float64): "
+          + ", ".join(f"({p}, {e:.2e}, {w:.2e})" for p, e, w in rows))
+    assert all(e <= 1.1 * w for _, e, w in rows), rows
+
+
 @pytest.mark.parametrize("world", [2, 8])
 def test_batch_tp_shard_step_nocomm(gpu, monkeypatch, world):
     """One rank of a C4-shaped tensor-parallel batch (Llama-3-8B shapes, 2 layers, batch 8): the rank's
