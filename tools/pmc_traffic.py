@@ -63,7 +63,7 @@ res[key] = {
 
 def family(k):
     """Kernel family of a decode-step dispatch (the names bench.py's roofline uses), or None."""
-    if "attn_partial_kernel" in k:
+    if "attn_partial_kernel" in k or "attn_mfma_kernel" in k:  # register path / MFMA GQA path (merge in-launch)
         return "attention"
     for tag, fam in (("EpiQKV", "qkv"), ("EpiSwiGLU", "gate_up"), ("EpiLogits", "lm_head")):
         if tag in k and weight_kernel(k):
