@@ -28,8 +28,6 @@ struct GemvIn {
     int cw = 16;     // waves per workgroup that stream (gemv_wave_count); the others only shadow loads
     int blk0 = 0;    // workgroups in front of the GEMV's own in the grid (qkv_attn.h: the attention's); OFFS only
     int blk1 = 0;    // OFFS: the end of the GEMV's workgroups (0: the grid's end)
-    int xrep = 1;         // > 1: x (and norm_w) are replicated xrep times, xrep_stride floats apart; workgroup b
-    int xrep_stride = 0;  // stages copy b % xrep (XStage): the chip's reads of one broadcast vector spread
 };
 
 constexpr int kGemvThreads = 1024;  // one persistent 16-wave workgroup per CU: x staged once per CU
@@ -76,10 +74,9 @@ struct XStage {
     float4 wr[kGemvStageV4];
     __device__ __forceinline__ void issue(const GemvIn& in) {
         const int tid = threadIdx.x, nt = kGemvThreads, n4 = in.cols >> 2;
-        const size_t rep = in.xrep > 1 ? (size_t)(blockIdx.x % (unsigned)in.xrep) * in.xrep_stride : 0;
-        const float4* x4 = reinterpret_cast<const float4*>(in.x + rep);
+        const float4* x4 = reinterpret_cast<const float4*>(in.x);
         // unconditional (clamped) loads: a load under a branch would make the weight waits conservative
-        const float4* w4 = reinterpret_cast<const float4*>(in.norm_w ? in.norm_w + rep : in.x + rep);
+        const float4* w4 = reinterpret_cast<const float4*>(in.norm_w ? in.norm_w : in.x);
 #pragma unroll
         for (int k = 0; k < kGemvStageV4; ++k) {
             xr[k] = x4[min(tid + k * nt, n4 - 1)];

@@ -564,99 +564,6 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
-    if (mode == "xrep") {
-        // the input vector (and norm weights) replicated XR times, workgroup b staging copy b % XR (GemvIn::xrep):
-        // does spreading the chip's 256 reads of one broadcast vector over XR copies shorten the input staging?
-        constexpr int XRMAX = 128, XSTR = 16384 + 64;
-        float *xr, *nwr;
-        CK(hipMalloc(&xr, sizeof(float) * XRMAX * XSTR));
-        CK(hipMalloc(&nwr, sizeof(float) * XRMAX * XSTR));
-        for (int r = 0; r < XRMAX; ++r) {
-            CK(hipMemcpy(xr + (size_t)r * XSTR, x, 16384 * 4, hipMemcpyDeviceToDevice));
-            CK(hipMemcpy(nwr + (size_t)r * XSTR, nw, 16384 * 4, hipMemcpyDeviceToDevice));
-        }
-        const int nst = 256 * 16 * 4;
-        unsigned long long* st;
-        CK(hipMalloc(&st, (size_t)NL * nst * 8));
-        std::vector<unsigned long long> h((size_t)NL * nst);
-        struct XC { const char* name; int si, rows, cols, R, U; bool norm, i8; };
-        const XC xc[] = {{"f16 qkv", 0, 12288, 4096, 2, 4, true, false}, {"f16 wo", 1, 4096, 4096, 1, 2, false, false},
-                         {"f16 gu", 2, 22016, 4096, 2, 4, true, false}, {"f16 down", 3, 4096, 11008, 1, 6, false, false},
-                         {"i8 qkv", 0, 12288, 4096, 2, 2, true, true}, {"i8 wo", 1, 4096, 4096, 1, 2, false, true},
-                         {"i8 down", 3, 4096, 11008, 1, 4, false, true}, {"tp8 qkv", 0, 1536, 4096, 2, 4, true, false},
-                         {"tp8 gu", 2, 2752, 4096, 2, 4, true, false}};
-        std::vector<float> ref(32768), got(32768);
-        for (const XC& t : xc) {
-            const long long bytes = (long long)t.rows * t.cols * (t.i8 ? 1 : 2);
-            const float s_ms = time_graph(s, [&] {
-                for (int l = 0; l < NL; ++l)
-                    hipLaunchKernelGGL(stream_kernel<8>, dim3(256), dim3(1024), 0, s, (const char*)w[t.si][l], bytes, y2,
-                                       nullptr);
-            });
-            for (int rep : {1, 8, 32, 128}) {
-                auto launch = [&](int l, unsigned long long* stp, float* out) {
-                    GemvIn in{xr, t.norm ? nwr : nullptr, 1e-5f, t.cols};
-                    in.stamps = stp;
-                    in.xrep = rep;
-                    in.xrep_stride = XSTR;
-                    if (t.i8) {
-                        const int8_t* W8 = (const int8_t*)w[t.si][l];
-                        if (t.R == 2) {
-                            EpiStore<2> e{out, nullptr, nullptr, 1.0f, t.rows};
-                            CK((launch_gemv_u<int8_t, 2, 2, true>(W8, in, e, t.rows / 2, s)));
-                        } else if (t.U == 2) {
-                            EpiStore<1> e{out, nullptr, nullptr, 1.0f, t.rows};
-                            CK((launch_gemv_u<int8_t, 1, 2, true>(W8, in, e, t.rows, s)));
-                        } else {
-                            EpiStore<1> e{out, nullptr, nullptr, 1.0f, t.rows};
-                            CK((launch_gemv_u<int8_t, 1, 4, true>(W8, in, e, t.rows, s)));
-                        }
-                    } else if (t.R == 2) {
-                        EpiStore<2> e{out, nullptr, nullptr, 1.0f, t.rows};
-                        CK((launch_gemv_u<__half, 2, 4, true>(w[t.si][l], in, e, t.rows / 2, s)));
-                    } else if (t.U == 2) {
-                        EpiStore<1> e{out, nullptr, nullptr, 1.0f, t.rows};
-                        CK((launch_gemv_u<__half, 1, 2, true>(w[t.si][l], in, e, t.rows, s)));
-                    } else {
-                        EpiStore<1> e{out, nullptr, nullptr, 1.0f, t.rows};
-                        CK((launch_gemv_u<__half, 1, 6, true>(w[t.si][l], in, e, t.rows, s)));
-                    }
-                };
-                launch(0, nullptr, rep == 1 ? y : y2);
-                CK(hipStreamSynchronize(s));
-                CK(hipMemcpy((rep == 1 ? ref : got).data(), rep == 1 ? y : y2, 4 * t.rows, hipMemcpyDeviceToHost));
-                if (rep > 1)
-                    for (int r = 0; r < t.rows; ++r)
-                        if (ref[r] != got[r]) {
-                            printf("MISMATCH %s xrep %d row %d\n", t.name, rep, r);
-                            break;
-                        }
-                const float g_ms = time_graph(s, [&] { for (int l = 0; l < NL; ++l) launch(l, nullptr, y); });
-                CK(hipMemset(st, 0, (size_t)NL * nst * 8));
-                time_graph(s, [&] { for (int l = 0; l < NL; ++l) launch(l, st + (size_t)l * nst, y); }, 1);
-                CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
-                std::vector<double> stg, ex;
-                for (int l = 2; l < NL; ++l) {
-                    const unsigned long long* q = h.data() + (size_t)l * nst;
-                    unsigned long long t0 = ~0ull;
-                    for (int i = 0; i < 4096; ++i)
-                        if (q[i * 4 + 3]) t0 = std::min(t0, q[i * 4]);
-                    for (int i = 0; i < 4096; ++i) {
-                        if (q[i * 4 + 3] == 0) continue;
-                        stg.push_back((q[i * 4 + 1] - t0) * 0.01);
-                        ex.push_back((q[i * 4 + 2] - t0) * 0.01);
-                    }
-                }
-                std::sort(stg.begin(), stg.end());
-                std::sort(ex.begin(), ex.end());
-                auto pc = [](std::vector<double>& v, double f) { return v.empty() ? 0.0 : v[(size_t)(f * (v.size() - 1))]; };
-                printf("%-9s xrep %3d  gemv %6.2f us  stream %6.2f us | staged p50 %5.2f p99 %5.2f | exit p50 %5.2f max %5.2f\n",
-                       t.name, rep, 1000.0 * g_ms / NL, 1000.0 * s_ms / NL, pc(stg, .5), pc(stg, .99), pc(ex, .5), pc(ex, 1.0));
-                fflush(stdout);
-            }
-        }
-        return 0;
-    }
     if (mode == "tp8") {
         // the TP-8 shard GEMVs as the engine launches them (launch_gemv_u: the column split at these sizes), per
         // launch phase stamps, beside the streaming-read floor of the same bytes: where a small launch's time goes
