@@ -44,6 +44,30 @@ __global__ void fill_f(float* p, size_t n, unsigned seed, float off) {
     }
 }
 
+
+// LAB_U=n: the kernel at a forced step width n (16-byte loads per lane per step) instead of bg_step_width's
+template <bool NORM, int U>
+static hipError_t launch_u(const __half* W, const BgIn& in_, const BgEpiStore& e, const BgPlan& p, hipStream_t s) {
+    static const hipError_t a = hipFuncSetAttribute(reinterpret_cast<const void*>(&bgemm_kernel<BgEpiStore, NORM, U>),
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize, kBgLdsMax);
+    if (a != hipSuccess) return a;
+    BgIn in = in_;
+    in.ntiles = p.ntiles;
+    in.tpw = p.tpw;
+    in.splits = p.splits;
+    hipLaunchKernelGGL((bgemm_kernel<BgEpiStore, NORM, U>), dim3(p.groups * p.splits), dim3(kBgThreads), p.lds, s, W, in, e);
+    return hipGetLastError();
+}
+static hipError_t lab_launch(const __half* W, const BgIn& in, const BgEpiStore& e, const BgPlan& p, hipStream_t s) {
+    const int u = getenv("LAB_U") ? atoi(getenv("LAB_U")) : 0;
+    const bool nrm = in.norm_w != nullptr;
+    if (u == 8) return nrm ? launch_u<true, 8>(W, in, e, p, s) : launch_u<false, 8>(W, in, e, p, s);
+    if (u == 6) return nrm ? launch_u<true, 6>(W, in, e, p, s) : launch_u<false, 6>(W, in, e, p, s);
+    if (u == 4) return nrm ? launch_u<true, 4>(W, in, e, p, s) : launch_u<false, 4>(W, in, e, p, s);
+    if (u == 2) return nrm ? launch_u<true, 2>(W, in, e, p, s) : launch_u<false, 2>(W, in, e, p, s);
+    return launch_bgemm(W, in, e, p, s);
+}
+
 static double time_cfg(const std::vector<__half*>& Ws, int rows, int K, int B, bool norm, BgPlan p, float* x,
                        float* nw, float* y, float* ws, unsigned* cnt, int reps) {
     hipStream_t s;
@@ -53,12 +77,12 @@ static double time_cfg(const std::vector<__half*>& Ws, int rows, int K, int B, b
     BgEpiStore e{y, nullptr, nullptr, 1.0f, rows, rows};
     CK((bg_allow_lds<BgEpiStore, true>()));
     CK((bg_allow_lds<BgEpiStore, false>()));
-    for (auto* W : Ws) CK(launch_bgemm(W, in, e, p, s));  // warm-up
+    for (auto* W : Ws) CK(lab_launch(W, in, e, p, s));  // warm-up
     CK(hipStreamSynchronize(s));
     hipGraph_t g;
     hipGraphExec_t ge;
     CK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
-    for (auto* W : Ws) CK(launch_bgemm(W, in, e, p, s));
+    for (auto* W : Ws) CK(lab_launch(W, in, e, p, s));
     CK(hipStreamEndCapture(s, &g));
     CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
     CK(hipGraphLaunch(ge, s));
@@ -145,7 +169,7 @@ int main(int argc, char** argv) {
             BgIn in{x, sh.norm ? nw : nullptr, 1e-5f, sh.K, B, 0, 0, 0, ws, cnt, st};
             in.tiled = getenv("LAB_TILED") ? 1 : 0;
             BgEpiStore e{y, nullptr, nullptr, 1.0f, sh.rows, sh.rows};
-            CK(launch_bgemm(Ws[0], in, e, p, 0));
+            CK(lab_launch(Ws[0], in, e, p, 0));
             CK(hipDeviceSynchronize());
             std::vector<unsigned long long> h(4 * nwg);
             CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
