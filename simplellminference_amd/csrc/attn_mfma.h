@@ -431,11 +431,16 @@ __global__ void __launch_bounds__(64 * kAmWaves) attn_mfma_kernel(AttnArgs<__hal
 }
 
 // Tiles per wave for a launch over n_kv kv heads (every sequence's) of a T-position cache: one workgroup per CU
-// over the whole context where the cache is long enough, at least one tile per wave.
+// over the whole context where the cache is long enough, at least one tile per wave, and at most kAmMaxSplits
+// splits per kv head: the last arriver's merge grows with the split count (its arrivals serialise on one counter),
+// 6.6 us at 32 splits against 3.7 at 16 — C4's TP-8 shard (8 kv heads, ctx 4096) at 16 splits on 128 workgroups
+// takes 11.9 us instead of 13.3 on 256 (tools/attn_mfma_lab, profiles/r5_attn_mfma_tpw.txt).
+constexpr int kAmMaxSplits = 16;
 inline int attn_mfma_tpw(int n_kv, int T, int cus) {
     const long long keys = (long long)n_kv * T;
     const long long per = (keys + cus - 1) / cus;  // keys per CU
     int tpw = (int)((per + kAmWgKeys / 2) / kAmWgKeys);
+    tpw = std::max(tpw, (T + kAmWgKeys * kAmMaxSplits - 1) / (kAmWgKeys * kAmMaxSplits));
     return tpw < 1 ? 1 : tpw > 64 ? 64 : tpw;
 }
 

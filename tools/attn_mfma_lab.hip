@@ -230,5 +230,9 @@ int main(int argc, char** argv) {
     run<128, 4>("B1-8B", 8, 8, 4096, {4095}, 16, 0, 0);
     run<128, 1>("C2-tp8", 4, 4, 2048, {2047}, 16, 0, 0);
     run<128, 4>("C4-tp8", 8, 1, 4096, {4095}, 16, 2, 0);
+    for (int t : {2, 4}) {  // small grids: fewer, longer splits (a shorter last-arriver merge)
+        run<128, 4>("C4-tp8-t", 8, 1, 4096, {4095}, 16, 2, 0, t);
+        run<128, 4>("B1-8B-t", 8, 8, 4096, {4095}, 16, 0, 0, t);
+    }
     return 0;
 }
