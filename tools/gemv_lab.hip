@@ -564,6 +564,48 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
+    if (mode == "split15") {
+        // q/k/v at 1.5 two-row units per wave (6144 units, 256 workgroups x 16 waves): the engine's unsplit launch
+        // (8 waves of 2 units, 8 of 1 per workgroup) against every unit cut in two column halves (SPLIT, CS 2) at the
+        // same U, i.e. 3 equal half-unit items per wave; fp16 U 4 and int8 U 2 (both 2 chunks per row)
+        std::vector<float> ref(32768), got(32768);
+        const int rows = 12288, cols = 4096;
+        for (int i8 = 0; i8 < 2; ++i8) {
+            for (int cs : {1, 2}) {
+                auto launch = [&](int l, float* out) {
+                    GemvIn in{x, nw, 1e-5f, cols};
+                    in.csplit = cs;
+                    EpiStore<2> e{out, nullptr, nullptr, 1.0f, rows};
+                    if (i8) {
+                        const int8_t* W8 = (const int8_t*)w[0][l];
+                        if (cs == 1) CK((launch_gemv<int8_t, 2, 2, true, EpiStore<2>, 2, false>(W8, in, e, rows / 2, s)));
+                        else CK((launch_gemv<int8_t, 2, 2, true, EpiStore<2>, 2, true>(W8, in, e, rows / 2, s)));
+                    } else {
+                        if (cs == 1) CK((launch_gemv<__half, 2, 4, true, EpiStore<2>, 2, false>(w[0][l], in, e, rows / 2, s)));
+                        else CK((launch_gemv<__half, 2, 4, true, EpiStore<2>, 2, true>(w[0][l], in, e, rows / 2, s)));
+                    }
+                };
+                launch(0, cs == 1 ? y : y2);
+                CK(hipStreamSynchronize(s));
+                CK(hipMemcpy((cs == 1 ? ref : got).data(), cs == 1 ? y : y2, 4 * rows, hipMemcpyDeviceToHost));
+                double md = 0;
+                if (cs > 1)
+                    for (int r = 0; r < rows; ++r) md = std::max(md, (double)std::fabs(ref[r] - got[r]));
+                for (int rep = 0; rep < 3; ++rep) {
+                    const float ms = time_graph(s, [&] { for (int l = 0; l < NL; ++l) launch(l, y); });
+                    printf("%s qkv cs %d  %7.2f us  (max|d| vs cs 1: %.2e)\n", i8 ? "i8 " : "f16", cs, 1000.0 * ms / NL, md);
+                }
+                fflush(stdout);
+            }
+            const long long bytes = (long long)rows * cols * (i8 ? 1 : 2);
+            const float sm = time_graph(s, [&] {
+                for (int l = 0; l < NL; ++l)
+                    hipLaunchKernelGGL(stream_kernel<8>, dim3(256), dim3(1024), 0, s, (const char*)w[0][l], bytes, y2, nullptr);
+            });
+            printf("%s qkv stream %7.2f us\n", i8 ? "i8 " : "f16", 1000.0 * sm / NL);
+        }
+        return 0;
+    }
     if (mode == "tp8") {
         // the TP-8 shard GEMVs as the engine launches them (launch_gemv_u: the column split at these sizes), per
         // launch phase stamps, beside the streaming-read floor of the same bytes: where a small launch's time goes
