@@ -126,7 +126,11 @@ def test_softmax(gpu, oracle, n):
 @pytest.mark.parametrize("kv_dtype", ["f32", "f16"])
 @pytest.mark.parametrize("T,hd,H,Hkv,layer,pos", [(64, 64, 4, 4, 1, 0), (64, 64, 4, 2, 0, 35), (64, 64, 4, 2, 1, 63),
                                                  (2048, 128, 32, 32, 0, 2047), (2048, 128, 32, 8, 1, 777),
-                                                 (300, 128, 8, 1, 0, 299)])
+                                                 (300, 128, 8, 1, 0, 299),
+                                                 # fp16: the MFMA kernel's split cap (one kv head, 16 splits of 256
+                                                 # keys), tile / split boundaries, hd 64 GQA-8
+                                                 (4096, 128, 4, 1, 0, 4095), (4096, 128, 4, 1, 1, 255),
+                                                 (4096, 128, 32, 8, 1, 1024), (4096, 64, 16, 2, 0, 129)])
 def test_mha(gpu, oracle, kv_dtype, T, hd, H, Hkv, layer, pos):
     torch = gpu
     from simplellminference_amd import ops
