@@ -131,6 +131,7 @@ int main(int argc, char** argv) {
         const double gb = n * 2.0 / 1e9;
         BgPlan auto_p = bg_plan(tiles, sh.K, B, sh.norm);
         std::vector<BgPlan> cands = {auto_p};
+
         const bool auto_only = getenv("LAB_AUTO_ONLY") != nullptr;
         const int tpws[] = {1, 2, 3, 4, 6, 8, 12, 16, 24, 32};
         const int sps[] = {1, 2, 4, 8};
@@ -160,9 +161,9 @@ int main(int argc, char** argv) {
                    c == 0 ? "AUTO" : "    ", p.tpw, p.splits, p.groups * p.splits, us, gb / (us * 1e-6), us_nn);
             fflush(stdout);
         }
-        {  // per-workgroup phase stamps (s_memrealtime, 100 MHz) of one launch of the AUTO plan
+        for (size_t ci = 0; ci < 1; ++ci) {  // per-workgroup phase stamps (s_memrealtime, 100 MHz) of the AUTO plan
             unsigned long long* st;
-            const BgPlan& p = cands[0];
+            const BgPlan& p = cands[ci];
             const int nwg = p.groups * p.splits;
             CK(hipMalloc(&st, sizeof(unsigned long long) * 4 * nwg));
             CK(hipMemset(st, 0, sizeof(unsigned long long) * 4 * nwg));
@@ -183,9 +184,19 @@ int main(int argc, char** argv) {
                 if (h[4 * i + 3]) ep_sum += h[4 * i + 3] - h[4 * i + 2];
                 tmax = std::max(tmax, std::max(h[4 * i + 2], h[4 * i + 3]));
             }
-            printf("   stamps: entry spread %.2f us, staging avg %.2f us, stream avg %.2f us, epilogue avg %.2f us, "
-                   "first entry -> last end %.2f us\n", ent_max / 100.0, st_sum / nwg / 100.0, str_sum / nwg / 100.0,
+            printf("   %s stamps: entry spread %.2f us, staging avg %.2f us, stream avg %.2f us, epilogue avg %.2f us, "
+                   "first entry -> last end %.2f us\n", "AUTO", ent_max / 100.0, st_sum / nwg / 100.0, str_sum / nwg / 100.0,
                    ep_sum / nwg / 100.0, (tmax - t0) / 100.0);
+            std::vector<double> send, eend;  // per workgroup: stream end, epilogue end (us after the first entry)
+            for (int i = 0; i < nwg; ++i) {
+                send.push_back((h[4 * i + 2] - t0) / 100.0);
+                if (h[4 * i + 3]) eend.push_back((h[4 * i + 3] - t0) / 100.0);
+            }
+            std::sort(send.begin(), send.end());
+            std::sort(eend.begin(), eend.end());
+            auto pc = [](const std::vector<double>& v, double f) { return v.empty() ? 0.0 : v[(size_t)(f * (v.size() - 1))]; };
+            printf("   stream end p10 %.2f p50 %.2f p90 %.2f max %.2f | epilogue end (%zu wg) p50 %.2f max %.2f us\n",
+                   pc(send, .1), pc(send, .5), pc(send, .9), pc(send, 1.0), eend.size(), pc(eend, .5), pc(eend, 1.0));
             CK(hipFree(st));
         }
         for (auto* W : Ws) CK(hipFree(W));
