@@ -606,6 +606,49 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
+    if (mode == "downcs") {
+        // the 7B down GEMV (4096 rows x 11008 cols fp16, 1376 vectors per row: U 6 leaves the 4th chunk 58 % full)
+        // unsplit (the engine) against each row cut in two / four column parts (SPLIT): 2 / 4 items per wave
+        std::vector<float> ref(32768), got(32768);
+        const int rows = 4096, cols = 11008;
+        struct V { int cs, u; };
+        for (V v : {V{1, 6}, V{2, 6}, V{2, 4}, V{4, 4}, V{4, 2}, V{1, 8}, V{2, 8}}) {
+            auto launch = [&](int l, float* out) {
+                GemvIn in{x, nullptr, 1e-5f, cols};
+                in.csplit = v.cs;
+                EpiStore<1> e{out, nullptr, nullptr, 1.0f, rows};
+#define DCS(U_)                                                                                                 \
+    do {                                                                                                        \
+        if (v.cs == 1) CK((launch_gemv<__half, 1, U_, true, EpiStore<1>, 2, false>(w[3][l], in, e, rows, s)));   \
+        else CK((launch_gemv<__half, 1, U_, true, EpiStore<1>, 2, true>(w[3][l], in, e, rows, s)));              \
+    } while (0)
+                if (v.u == 6) DCS(6);
+                else if (v.u == 4) DCS(4);
+                else if (v.u == 8) DCS(8);
+                else DCS(2);
+#undef DCS
+            };
+            const bool base = v.cs == 1 && v.u == 6;
+            launch(0, base ? y : y2);
+            CK(hipStreamSynchronize(s));
+            CK(hipMemcpy((base ? ref : got).data(), base ? y : y2, 4 * rows, hipMemcpyDeviceToHost));
+            double md = 0;
+            if (!base)
+                for (int r = 0; r < rows; ++r) md = std::max(md, (double)std::fabs(ref[r] - got[r]));
+            for (int rep = 0; rep < 3; ++rep) {
+                const float ms = time_graph(s, [&] { for (int l = 0; l < NL; ++l) launch(l, y); });
+                printf("f16 down cs %d U %d  %7.2f us  (max|d| vs cs 1 U 6: %.2e)\n", v.cs, v.u, 1000.0 * ms / NL, md);
+            }
+            fflush(stdout);
+        }
+        const float sm = time_graph(s, [&] {
+            for (int l = 0; l < NL; ++l)
+                hipLaunchKernelGGL(stream_kernel<8>, dim3(256), dim3(1024), 0, s, (const char*)w[3][l],
+                                   (long long)rows * cols * 2, y2, nullptr);
+        });
+        printf("f16 down stream %7.2f us\n", 1000.0 * sm / NL);
+        return 0;
+    }
     if (mode == "tp8") {
         // the TP-8 shard GEMVs as the engine launches them (launch_gemv_u: the column split at these sizes), per
         // launch phase stamps, beside the streaming-read floor of the same bytes: where a small launch's time goes
