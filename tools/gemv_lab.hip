@@ -249,101 +249,6 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
-    if (mode == "dma") {
-        // streaming-read floor: register loads (stream_kernel, 8 x 16 B per lane in flight, 1024 threads) against
-        // LDS-DMA rings (S KiB per wave, nt or default policy, 256 / 512 / 1024 threads), on the gate/up and down
-        // matrices (fp16 7B: 180 / 90 MB), each over NL distinct layers in a graph
-        for (int si : {2, 3, 0}) {
-            const long long bytes = (long long)kShapes[si].rows * kShapes[si].cols * 2;
-            auto rep = [&](const char* name, const std::function<void(int)>& f) {
-                for (int r = 0; r < 2; ++r) {
-                    const float ms = time_graph(s, [&] { for (int l = 0; l < NL; ++l) f(l); });
-                    const double us = 1000.0 * ms / NL;
-                    printf("%-5s %-24s %7.2f us  %7.1f GB/s\n", kShapes[si].name, name, us, bytes / (us * 1e-6) / 1e9);
-                }
-                fflush(stdout);
-            };
-            rep("reg 8x16B 1024t", [&](int l) {
-                hipLaunchKernelGGL(stream_kernel<8>, dim3(256), dim3(1024), 0, s, (const char*)w[si][l], bytes, y2, nullptr);
-            });
-#define DMA_CFG(NAME, S_, NT_, THREADS)                                                                          \
-            {                                                                                                \
-                const size_t lds = (size_t)(THREADS / 64) * S_ * 1024;                                        \
-                CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&stream_dma_kernel<S_, NT_>),             \
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));              \
-                rep(NAME, [&](int l) {                                                                        \
-                    hipLaunchKernelGGL((stream_dma_kernel<S_, NT_>), dim3(256), dim3(THREADS), lds, s,           \
-                                       (const char*)w[si][l], bytes, y2);                                      \
-                });                                                                                           \
-            }
-            DMA_CFG("dma nt S8 1024t", 8, true, 1024)
-            DMA_CFG("dma nt S9 1024t", 9, true, 1024)
-            DMA_CFG("dma nt S16 512t", 16, true, 512)
-            DMA_CFG("dma nt S32 256t", 32, true, 256)
-            DMA_CFG("dma nt S36 256t", 36, true, 256)
-            DMA_CFG("dma def S8 1024t", 8, false, 1024)
-            DMA_CFG("dma def S32 256t", 32, false, 256)
-#undef DMA_CFG
-        }
-        return 0;
-    }
-    if (mode == "gdma") {
-        // the fp16 GEMV with its weight stream in LDS-DMA rings (gemv_dma.h) against the register GEMV (gemv.h, the
-        // engine's R / U) on the 7B shapes; max |difference| of the outputs, then graph-replay times
-        std::vector<float> ref(32768), got(32768);
-        struct GC { const char* name; int si, rows, cols; bool norm; };
-        const GC gc[] = {{"gu", 2, 22016, 4096, true}, {"down", 3, 4096, 11008, false}, {"qkv", 0, 12288, 4096, true},
-                         {"lm", 4, 32000, 4096, true}};
-        for (const GC& t : gc) {
-            const int nl = t.si == 4 ? 4 : NL;
-            auto reg = [&](int l, float* out) {
-                GemvIn in{x, t.norm ? nw : nullptr, 1e-5f, t.cols};
-                if (t.si == 3) {
-                    EpiStore<1> e{out, nullptr, nullptr, 1.0f, t.rows};
-                    CK((launch_gemv<__half, 1, 6, true>(w[t.si][l], in, e, t.rows, s)));
-                } else {
-                    EpiStore<2> e{out, nullptr, nullptr, 1.0f, t.rows};
-                    CK((launch_gemv<__half, 2, 4, true>(w[t.si][l], in, e, t.rows / 2, s)));
-                }
-            };
-            std::vector<std::pair<const char*, std::function<void(int, float*)>>> vs;
-            vs.push_back({"register", reg});
-#define GD(NAME, U_, NSW_, S2_, S1_)                                                                              \
-            vs.push_back({NAME, [&](int l, float* out) {                                                      \
-                GemvIn in{x, t.norm ? nw : nullptr, 1e-5f, t.cols};                                           \
-                if (t.si == 3) {                                                                              \
-                    EpiStore<1> e{out, nullptr, nullptr, 1.0f, t.rows};                                       \
-                    CK((launch_gemv_dma<1, U_, NSW_, S1_>(w[t.si][l], in, e, t.rows, s)));                     \
-                } else {                                                                                      \
-                    EpiStore<2> e{out, nullptr, nullptr, 1.0f, t.rows};                                       \
-                    CK((launch_gemv_dma<2, U_, NSW_, S2_>(w[t.si][l], in, e, t.rows / 2, s)));                 \
-                }                                                                                             \
-            }});
-            GD("dma U4 4w x 32 KiB", 4, 4, 32, 24)
-            GD("dma U2 8w x 16 KiB", 2, 8, 16, 14)
-            GD("dma U4 8w x 16 KiB", 4, 8, 16, 12)
-            GD("dma U2 4w x 32 KiB", 2, 4, 32, 28)
-            GD("dma U2 16w x 8 KiB", 2, 16, 8, 8)
-#undef GD
-            for (size_t v = 0; v < vs.size(); ++v) {
-                vs[v].second(0, v == 0 ? y : y2);
-                CK(hipStreamSynchronize(s));
-                CK(hipMemcpy((v == 0 ? ref : got).data(), v == 0 ? y : y2, 4 * t.rows, hipMemcpyDeviceToHost));
-                double md = 0, mr = 0;
-                if (v > 0)
-                    for (int r = 0; r < t.rows; ++r) {
-                        md = std::max(md, (double)std::fabs(ref[r] - got[r]));
-                        mr = std::max(mr, (double)std::fabs(ref[r]));
-                    }
-                for (int rep = 0; rep < 2; ++rep) {
-                    const float ms = time_graph(s, [&] { for (int l = 0; l < nl; ++l) vs[v].second(l, y); });
-                    printf("%-5s %-22s %7.2f us  (max|d| %.2e of max|y| %.2e)\n", t.name, vs[v].first, 1000.0 * ms / nl, md, mr);
-                }
-                fflush(stdout);
-            }
-        }
-        return 0;
-    }
     if (mode == "mall") {
         // wo GEMV (R1U2) timed cold (distinct layers) and right after a streaming read of the same matrix
         // (Infinity-Cache hot): is a prefetch in an earlier launch worth anything to the GEMV?
