@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <functional>
 #include <vector>
 
 #include "../simplellminference_amd/csrc/attn_mfma.h"
@@ -208,8 +209,137 @@ static void run(const char* name, int nkv, int seq_heads, int T, std::vector<int
     CK(hipFree(st));
 }
 
+
+// K/V warm-up by plain (default-policy, Infinity-Cache allocating) loads: attention workgroup aw (kv head aw / splits,
+// split aw % splits) gets its first nk keys' K and V rows read; one prefetch workgroup covers per_wg of them
+template <int HD>
+__global__ void __launch_bounds__(1024) kv_prefetch_kernel(const __half* K, const __half* V, int T, int splits, int ppwg,
+                                                           int nk, int per_wg, int n_aw, float* sink) {
+    float acc = 0.0f;
+    const int chunks = nk * HD * 2 / 16;  // 16-byte chunks of one head's nk rows
+    for (int a = 0; a < per_wg; ++a) {
+        const int aw = blockIdx.x * per_wg + a;
+        if (aw >= n_aw) break;
+        const int h = aw / splits, sp = aw - h * splits;
+        const size_t base = ((size_t)h * T + (size_t)sp * ppwg) * HD * 2;  // bytes
+        for (int c = threadIdx.x; c < 2 * chunks; c += blockDim.x) {
+            const char* src = reinterpret_cast<const char*>(c < chunks ? K : V) + base + (size_t)(c % chunks) * 16;
+            const uint4 v = *reinterpret_cast<const uint4*>(src);
+            acc += __uint_as_float(v.x ^ v.w);
+        }
+    }
+    if (acc == 1.2345f) sink[threadIdx.x] = acc;
+}
+__global__ void __launch_bounds__(1024) nt_stream_kernel(const char* p, long long bytes, float* sink) {
+    const long long per = bytes / gridDim.x;
+    const char* b = p + per * blockIdx.x;
+    const int nvec = (int)(per / 16);
+    float acc = 0.0f;
+    for (int v = threadIdx.x; v < nvec; v += 8 * 1024) {
+        u32x4 w[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w[j] = load16<true>(b + (size_t)min(v + j * 1024, nvec - 1) * 16);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc += __uint_as_float(w[j].x ^ w[j].w);
+    }
+    if (acc == 1.2345f) sink[threadIdx.x] = acc;
+}
+
+// Does warming the first nk keys of every attention workgroup's split into the Infinity Cache (during the q/k/v
+// projection: a 50 MB nt stream stands in for it) shorten the C4 attention? Graph replays of NL layers.
+static void prefetch_test() {
+    constexpr int HD = 128, G = 4;
+    const int nkv = 64, T = 4096, NL = 3;
+    const int tpw = attn_mfma_tpw(nkv, T, cus());
+    const int ppwg = kAmWgKeys * tpw, splits = (T + ppwg - 1) / ppwg, blocks = nkv * splits;
+    const size_t per = (size_t)nkv * T * HD;
+    std::vector<__half*> K(NL), V(NL);
+    std::vector<char*> Wq(NL);
+    const long long wbytes = 50331648;  // the C4 q/k/v matrix
+    for (int l = 0; l < NL; ++l) {
+        CK(hipMalloc(&K[l], per * 2));
+        CK(hipMalloc(&V[l], per * 2));
+        CK(hipMalloc(&Wq[l], wbytes));
+        fill_h<<<1024, 256>>>(K[l], per, 3 + l);
+        fill_h<<<1024, 256>>>(V[l], per, 7 + l);
+        CK(hipMemset(Wq[l], 1, wbytes));
+    }
+    float *q, *out, *part, *sink;
+    unsigned* cnt;
+    int32_t* posd;
+    CK(hipMalloc(&q, sizeof(float) * nkv * G * HD));
+    CK(hipMalloc(&out, sizeof(float) * nkv * G * HD));
+    CK(hipMalloc(&part, sizeof(float) * (size_t)nkv * G * splits * (HD + kAttnPartPad)));
+    CK(hipMalloc(&cnt, sizeof(unsigned) * nkv));
+    CK(hipMemset(cnt, 0, sizeof(unsigned) * nkv));
+    CK(hipMalloc(&sink, 4096 * 4));
+    CK(hipMalloc(&posd, sizeof(int32_t) * 8 * 16));
+    std::vector<int32_t> hp(8 * 16, 0);
+    for (int b = 0; b < 8; ++b) hp[b * 16] = T - 1;
+    CK(hipMemcpy(posd, hp.data(), hp.size() * 4, hipMemcpyHostToDevice));
+    fill_f<<<64, 256>>>(q, (size_t)nkv * G * HD, 11, 2.0f);
+    CK(hipDeviceSynchronize());
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    auto attn = [&](int l) {
+        AttnArgs<__half> a{q, K[l], V[l], HD, (long long)T * HD, part, out, cnt, posd, 0, nkv, splits,
+                           1.0f / sqrtf((float)HD), 8, 16, nullptr};
+        a.defer_merge = 0;
+        a.ppwg = ppwg;
+        launch_mfma<HD, G>(a, blocks, 2, s);
+    };
+    auto strm = [&](int l) { hipLaunchKernelGGL(nt_stream_kernel, dim3(192), dim3(1024), 0, s, Wq[l], wbytes, sink); };
+    auto timed = [&](const std::function<void(int)>& body) {
+        hipGraph_t g;
+        hipGraphExec_t ge;
+        CK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
+        for (int l = 0; l < NL; ++l) body(l);
+        CK(hipStreamEndCapture(s, &g));
+        CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+        CK(hipGraphLaunch(ge, s));
+        CK(hipStreamSynchronize(s));
+        hipEvent_t e0, e1;
+        CK(hipEventCreate(&e0));
+        CK(hipEventCreate(&e1));
+        const int reps = 20;
+        CK(hipEventRecord(e0, s));
+        for (int r = 0; r < reps; ++r) CK(hipGraphLaunch(ge, s));
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        CK(hipGraphExecDestroy(ge));
+        CK(hipGraphDestroy(g));
+        return 1000.0 * ms / (reps * NL);
+    };
+    for (int rep = 0; rep < 2; ++rep) {
+        const double a0 = timed(attn), s0 = timed(strm), sa = timed([&](int l) { strm(l); attn(l); });
+        printf("attention alone %.2f us | 50 MB nt stream %.2f | stream + attention %.2f (attention ~%.2f)\n", a0, s0, sa,
+               sa - s0);
+        for (int nk : {64, 128, 256}) {
+            for (int pwg : {64, 32}) {
+                const int per_wg = (blocks + pwg - 1) / pwg;
+                auto pf = [&](int l) {
+                    hipLaunchKernelGGL((kv_prefetch_kernel<HD>), dim3(pwg), dim3(1024), 0, s, K[l], V[l], T, splits, ppwg, nk,
+                                       per_wg, blocks, sink);
+                };
+                const double p0 = timed(pf), ps = timed([&](int l) { pf(l); strm(l); }),
+                             psa = timed([&](int l) { pf(l); strm(l); attn(l); }),
+                             pa = timed([&](int l) { pf(l); attn(l); });
+                printf("  warm %3d keys/split by %2d wg: warm %.2f | warm+stream %.2f | warm+stream+attn %.2f (attention ~%.2f) | "
+                       "warm+attn %.2f (attention ~%.2f)\n", nk, pwg, p0, ps, psa, psa - ps, pa, pa - p0);
+                fflush(stdout);
+            }
+        }
+    }
+}
+
 int main(int argc, char** argv) {
     const int only_tpw = argc > 1 ? atoi(argv[1]) : 0;
+    if (only_tpw < 0) {  // tools/attn_mfma_lab -1: the Infinity-Cache warm-up test only
+        prefetch_test();
+        return 0;
+    }
     // correctness sweep (positions around tile / wave / split boundaries), then the timed shapes
     for (int p : {0, 1, 31, 32, 127, 128, 129, 255, 256, 300, 1023, 1024, 2047})
         run<128, 1>("C1-pos", 32, 32, 2048, {p}, 1, 1, 1);
