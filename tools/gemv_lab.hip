@@ -539,6 +539,15 @@ int main(int argc, char** argv) {
         I8_CFG("i8 down R1U4NB3", 3, false, 1, 4, 3);
         I8_CFG("i8 down R1U2NB4", 3, false, 1, 2, 4);
         I8_CFG("i8 down R2U2NB2", 3, false, 2, 2, 2);
+        // round 5: whole rows per step (int8 4096 columns = 256 vectors = one U 4 chunk)
+        I8_CFG("i8 qkv R2U4NB2", 0, true, 2, 4, 2);
+        I8_CFG("i8 gu R2U4NB2", 2, true, 2, 4, 2);
+        I8_CFG("i8 gu R1U4NB2", 2, true, 1, 4, 2);
+        I8_CFG("i8 wo R1U2NB2", 1, false, 1, 2, 2);
+        I8_CFG("i8 wo R1U4NB2", 1, false, 1, 4, 2);
+        I8_CFG("i8 wo R2U4NB2", 1, false, 2, 4, 2);
+        I8_CFG("i8 down R1U8NB2", 3, false, 1, 8, 2);
+
 #undef I8_CFG
         return 0;
     }
