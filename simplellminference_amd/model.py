@@ -4,7 +4,8 @@ over the fused, graph-captured HIP decode step of libsli.so (engine.hip).
 Differences from the reference, all deliberate and documented in DESIGN.md:
   * the model shape is a runtime ``LlamaModelConfig`` (the reference hard-codes config.h:5-17 and
     copies it back in read_model_file, model.cpp:219-230);
-  * ``predict`` takes token ids (the sentencepiece tokenizer, encode.cpp:5-27, is out of scope);
+  * ``predict`` takes token ids, or text when a ``tokenizer_path`` is given (``encode.SPELayer`` over the Python
+    sentencepiece package, encode.cpp:5-27; loaded in ``init`` as create_nonparam_layers does, model.cpp:328);
   * weights are either the reference's flat fp32 file (model_path) or seeded synthetic weights.
 """
 from __future__ import annotations
@@ -75,6 +76,7 @@ class LlamaModel:
         self.seed = seed
         self.batch = batch  # sequences decoding in lockstep (extension: the reference is batch 1)
         self._h = None
+        self.encode_layer = None
 
     # ------------------------------------------------------------------ model.h:63-67
     def _config_struct(self) -> ModelConfig:
@@ -87,6 +89,9 @@ class LlamaModel:
                            self.batch)
 
     def init(self) -> "LlamaModel":
+        if self.tokenizer_path:  # model.cpp:328 (RuntimeError when the model file does not load, encode.cpp:8-10)
+            from .encode import SPELayer
+            self.encode_layer = SPELayer(self.tokenizer_path)
         mc = self._config_struct()
         h = ctypes.c_void_p()
         cid = ctypes.create_string_buffer(self.comm_id, len(self.comm_id)) if self.comm_id else None
@@ -221,12 +226,32 @@ class LlamaModel:
 
     # ------------------------------------------------------------------ model.cpp:142-187
     def predict(self, prompt_ids, max_length: int, want_logits: bool = False):
+        """Token ids in: the tokens fed at positions 0..max_length-1 (and the logits). Text in (the reference's
+        ``predict(const std::string prompt, int max_length)``): encode it, run the same loop, print and return
+        the text model.cpp:154-186 writes — every fed token and the final argmax, decoded one by one."""
+        if isinstance(prompt_ids, str):
+            return self._predict_text(prompt_ids, max_length)
         p = np.ascontiguousarray(prompt_ids, np.int32)
         toks = np.empty(max_length, np.int32)
         logits = np.empty((max_length, self.local_vocab), np.float32) if want_logits else None
         call("sli_model_predict", self._h, p.ctypes.data_as(ctypes.c_void_p), p.size, max_length,
              toks.ctypes.data_as(ctypes.c_void_p), logits.ctypes.data_as(ctypes.c_void_p) if want_logits else None)
         return (toks, logits) if want_logits else toks
+
+    def _predict_text(self, prompt: str, max_length: int) -> str:
+        from .encode import render_predict
+        if self.encode_layer is None:
+            raise RuntimeError("predict(text) needs a tokenizer_path")
+        ids = self.encode_layer.encode(prompt)
+        if not ids:
+            raise ValueError("the prompt encodes to no tokens")
+        if max_length <= 0:  # the loop body never runs: only the first prompt token is printed (model.cpp:154-155)
+            text = render_predict(self.encode_layer, [], ids[0])
+        else:
+            fed = self.predict(ids, max_length)
+            text = render_predict(self.encode_layer, fed.reshape(-1, max_length)[0], self.state()["token"])
+        print(text, end="")
+        return text
 
     def prefill(self, prompt_ids):
         """Run prompt positions 0..n-2 through the layers in chunks of up to 256 (MFMA GEMM projections,
