@@ -26,6 +26,13 @@ namespace sli {
 constexpr int kOsMaxRanks = 8;
 constexpr unsigned kOsSpinLimit = 1u << 24;  // bounded wait (~seconds): gives up with DevState::error bit 4
 constexpr int kOsErrTimeout = 4;
+// A wait that has spun 4096 times looks at DevState::error: once one exchange of this process gave up (a peer that
+// never arrives), every later one gives up at once instead of after its own kOsSpinLimit — a broken exchange then
+// costs one timeout, not one per launch (bench.py's RCCL validation falls back within seconds).
+__device__ __forceinline__ bool os_gave_up(DevState* st, unsigned spins) {
+    return (spins & 4095u) == 4095u &&
+           (__hip_atomic_load(&st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & kOsErrTimeout) != 0;
+}
 // Per-workgroup exchanges (EpiPush::wg_mode, oneshot_sliced_kernel): flags [region 3][par 2][kOsMaxWg][kOsMaxRanks]
 // u32 after the 256-B header of the launch-level flags, then the data blocks of 8 slots x nmax floats: launch-level
 // par 0 / 1, then region 0 (batch-1 wo) par 0 / 1, region 1 (batch-1 down), region 2 (the sliced launch), region 3
@@ -89,7 +96,7 @@ __device__ __forceinline__ void os_finish(const OneShotArgs& a, char* const* pee
     if (tid < a.nranks) {
         unsigned* f = os_flag(peers[a.rank], par, tid);
         for (unsigned spins = 0; __hip_atomic_load(f, kAcq, __HIP_MEMORY_SCOPE_SYSTEM) != e; ++spins) {
-            if (spins >= kOsSpinLimit) {
+            if (spins >= kOsSpinLimit || os_gave_up(a.st, spins)) {
                 __hip_atomic_fetch_or(&a.st->error, kOsErrTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 *abort_lds = 1;
                 break;
@@ -195,7 +202,7 @@ __global__ void __launch_bounds__(256) oneshot_sliced_kernel(OneShotArgs a, char
     if (tid < a.nranks) {
         const unsigned* f = os_wg_flag(peer_tab[a.rank], 2, par, w, tid);
         for (unsigned spins = 0; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e; ++spins) {
-            if (spins >= kOsSpinLimit) {
+            if (spins >= kOsSpinLimit || os_gave_up(a.st, spins)) {
                 __hip_atomic_fetch_or(&a.st->error, kOsErrTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 abort = 1;
                 break;
@@ -272,7 +279,7 @@ struct BgEpiPush {
         if (tid < os.nranks) {
             const unsigned* f = os_wg_flag(peer_tab[os.rank], region, par, g, tid);
             for (unsigned spins = 0; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e; ++spins) {
-                if (spins >= kOsSpinLimit) {
+                if (spins >= kOsSpinLimit || os_gave_up(os.st, spins)) {
                     __hip_atomic_fetch_or(&os.st->error, kOsErrTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     *abort_lds = 1;
                     break;
@@ -388,7 +395,7 @@ struct EpiPush {
         if (tid < os.nranks) {
             const unsigned* f = os_wg_flag(peer_tab[os.rank], region, par, blockIdx.x, tid);
             for (unsigned spins = 0; __hip_atomic_load(f, kAcq, __HIP_MEMORY_SCOPE_SYSTEM) != e; ++spins) {
-                if (spins >= kOsSpinLimit) {
+                if (spins >= kOsSpinLimit || os_gave_up(os.st, spins)) {
                     __hip_atomic_fetch_or(&os.st->error, kOsErrTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     sh[1] = 1;
                     break;
