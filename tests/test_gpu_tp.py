@@ -287,3 +287,67 @@ def test_oneshot_allreduce_more_ranks(gpu, oracle, name, world, mode, w):
         otoks, ologits = _oracle_for(oracle, name, oracle.W_F16 if w == "f16" else oracle.W_I8, True).predict(PROMPT, 16)
         assert np.array_equal(toks, otoks)
         assert np.abs(logits - ologits).max() <= 1e-3
+
+
+def _absent_peer_rank(rank, world, port, q):
+    """Rank 0 steps with the fused exchange while rank 1 never does: rank 0's first wait gives up after the bounded
+    spin, every later one at once (oneshot.h os_gave_up)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0",
+                      SLI_DEBUG_NOCOMM="1")
+    import time
+
+    import torch.distributed as dist
+
+    from simplellminference_amd import SliError, tp
+    from simplellminference_amd.model import LlamaModel, preset
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m = LlamaModel(config=preset("tiny"), w_dtype="f16", kv_dtype="f16", tp_rank=rank, tp_size=world, seed=0).init()
+        tp.open_oneshot(m)
+        m.set_allreduce("fused")
+        dist.barrier()
+        if rank == 0:
+            def run(steps):  # steps x (2 layers x the wo / down exchanges + the argmax-key exchange)
+                t0 = time.perf_counter()
+                msg = ""
+                try:
+                    m.predict(PROMPT, steps)  # resets the state (and its error bits) first
+                except SliError as e:  # the device error check at the end of predict
+                    msg = str(e)
+                return time.perf_counter() - t0, msg
+            t1, msg1 = run(1)
+            t3, msg3 = run(3)
+            refused = False
+            try:
+                m.set_allreduce("oneshot")
+            except SliError:
+                refused = True
+            q.put(("ok", (t1, t3), (msg1, msg3), refused))
+        dist.barrier()  # rank 1 stays until rank 0 is done with the buffers it mapped
+        m.close()
+    except Exception as e:  # report to the parent instead of hanging it
+        q.put(("err", repr(e), None, None))
+    dist.destroy_process_group()
+
+
+def test_oneshot_absent_peer_gives_up_once(gpu):
+    """A peer that never arrives (rank 1 maps the buffers and does not step): rank 0's predict ends with
+    DevState::error bit 4 after ONE bounded wait, not one per exchange (oneshot.h os_gave_up: later waits give up
+    after 4096 polls): 3 steps take about as long as 1 (measured: 1 step, 5 exchanges, 2.57 s; 3 steps, 15 exchanges,
+    2.58 s). predict reports the timeout and the one-shot path is refused afterwards (os_dead), so bench.py falls
+    back to RCCL."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_absent_peer_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    status, times, msgs, refused = q.get(timeout=600)
+    for p in procs:
+        p.join(timeout=120)
+    assert status == "ok", times
+    assert all("one-shot all-reduce timed out" in msg for msg in msgs), msgs
+    t1, t3 = times
+    print(f"absent peer: 1 step (5 exchanges) {t1:.2f} s, 3 steps (15 exchanges) {t3:.2f} s")
+    assert t3 < 2.0 * t1  # one bounded wait each (3x that without the give-up)
+    assert refused
