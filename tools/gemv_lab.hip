@@ -105,6 +105,52 @@ __global__ void __launch_bounds__(1024) stream_dma_kernel(const char* p, long lo
     if (acc == 1.2345f) out[blockIdx.x] = acc;
 }
 
+// streaming read with a dynamic tail (mode "dyn"): workgroup b first reads its contiguous share of the first
+// static_frac of the bytes (as stream_kernel), then takes 16 x U KiB chunks of the rest from a counter (one
+// agent-scope add per chunk by thread 0, the next chunk's add issued while the current chunk's loads fly), so CUs
+// that finish their share early take more of the remainder. ctr: zero before the launch.
+template <int U>
+__global__ void __launch_bounds__(1024) stream_dyn_kernel(const char* p, long long bytes, float* out, unsigned* ctr,
+                                                          float static_frac) {
+    __shared__ int chunk_lds[2];
+    const long long st_bytes = ((long long)(bytes * static_frac) / (gridDim.x * 16384LL)) * gridDim.x * 16384LL;
+    const long long per = st_bytes / gridDim.x;
+    const char* b = p + per * blockIdx.x;
+    const int nvec = (int)(per / 16);
+    float acc = 0.0f;
+    // the first dynamic chunk's index, requested before the static share streams
+    if (threadIdx.x == 0) chunk_lds[0] = (int)__hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int v = threadIdx.x; v < nvec; v += U * 1024) {
+        u32x4 w[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) w[j] = load16<true>(b + (size_t)min(v + j * 1024, nvec - 1) * 16);
+#pragma unroll
+        for (int j = 0; j < U; ++j) acc += __uint_as_float(w[j].x ^ w[j].y ^ w[j].z ^ w[j].w);
+    }
+    const long long chunk = 1024LL * U * 16;
+    const long long rest = bytes - st_bytes;
+    const int nchunks = (int)((rest + chunk - 1) / chunk);
+    const char* d = p + st_bytes;
+    __syncthreads();
+    int c = chunk_lds[0];
+    int par = 0;
+    while (c < nchunks) {
+        if (threadIdx.x == 0)
+            chunk_lds[par ^ 1] = (int)__hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const long long base = (long long)c * chunk;
+        const int nv = (int)(min(chunk, rest - base) / 16);
+        u32x4 w[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) w[j] = load16<true>(d + base + (size_t)min((int)threadIdx.x + j * 1024, nv - 1) * 16);
+#pragma unroll
+        for (int j = 0; j < U; ++j) acc += __uint_as_float(w[j].x ^ w[j].y ^ w[j].z ^ w[j].w);
+        __syncthreads();
+        par ^= 1;
+        c = chunk_lds[par];
+    }
+    if (acc == 1.2345f) out[blockIdx.x] = acc;
+}
+
 // latency probe: wave 0 times one L2-hot load while the other 15 waves of the CU have `nw` 16-byte HBM
 // loads per lane in flight (nw = 0: idle CU). scalar = 1: wave 0 uses a scalar (s_load) read instead.
 __global__ void __launch_bounds__(1024) probe_kernel(const char* W, const float* x, int nw, int scalar,
@@ -246,6 +292,44 @@ int main(int argc, char** argv) {
             DMA_CFG("dma def S8 1024t", 8, false, 1024)
             DMA_CFG("dma def S32 256t", 32, false, 256)
 #undef DMA_CFG
+        }
+        return 0;
+    }
+    if (mode == "dyn") {
+        // static stream floor vs a dynamic tail (stream_dyn_kernel): does taking the last part of the bytes from a
+        // work counter shorten a launch's tail? NL distinct matrices per shape, in a graph (a memset zeroes the
+        // counters first).
+        unsigned* ctr;
+        CK(hipMalloc(&ctr, NL * 128));
+        for (int si : {0, 1, 2, 3}) {
+            const long long bytes = (long long)kShapes[si].rows * kShapes[si].cols * 2;
+            auto rep = [&](const char* name, const std::function<void(int)>& f) {
+                for (int r = 0; r < 2; ++r) {
+                    const float ms = time_graph(s, [&] {
+                        CK(hipMemsetAsync(ctr, 0, NL * 128, s));
+                        for (int l = 0; l < NL; ++l) f(l);
+                    });
+                    const double us = 1000.0 * ms / NL;
+                    printf("%-5s %-26s %7.2f us  %7.1f GB/s\n", kShapes[si].name, name, us, bytes / (us * 1e-6) / 1e9);
+                }
+                fflush(stdout);
+            };
+            rep("static reg 8x16B", [&](int l) {
+                hipLaunchKernelGGL(stream_kernel<8>, dim3(256), dim3(1024), 0, s, (const char*)w[si][l], bytes, y2, nullptr);
+            });
+            for (float fr : {0.95f, 0.85f, 0.7f, 0.5f}) {
+                char nm[64];
+                snprintf(nm, sizeof nm, "dyn U8 static %.2f", fr);
+                rep(nm, [&](int l) {
+                    hipLaunchKernelGGL(stream_dyn_kernel<8>, dim3(256), dim3(1024), 0, s, (const char*)w[si][l], bytes, y2,
+                                       ctr + l * 32, fr);
+                });
+                snprintf(nm, sizeof nm, "dyn U4 static %.2f", fr);
+                rep(nm, [&](int l) {
+                    hipLaunchKernelGGL(stream_dyn_kernel<4>, dim3(256), dim3(1024), 0, s, (const char*)w[si][l], bytes, y2,
+                                       ctr + l * 32, fr);
+                });
+            }
         }
         return 0;
     }
