@@ -10,7 +10,7 @@ DIRECTLY to the oracle's predict: tokens equal, logits within 1e-3), and one ran
 shards (2 layers, ctx 2048, head_dim 128, 8 splits per head; SLI_DEBUG_NOCOMM: the rank's own step, no exchange)
 at positions on and around the split and wave boundaries, each step run twice (the counters the launch leaves at
 zero must serve the next launch). The shards' fused steps are held to the oracle through the multi-process TP tests
-(test_gpu_tp.py, +qa), which compare whole TP steps with the exchange."""
+(test_gpu_tp.py, +qa, including Llama-2-7B's TP-4 shards), which compare whole TP steps with the exchange."""
 import json
 import os
 import subprocess

@@ -70,8 +70,7 @@ def test_rccl_tp2_matches_tp1(gpu, name):
 
 
 def _oracle_for(oracle, name, wmode, kv_f16):
-    from simplellminference_amd.model import preset
-    c = preset(name)
+    c = _preset(name)  # "preset:layers" too
     return oracle.Model(oracle.Config(c.vocab_size, c.hidden_size, c.num_attention_heads, c.num_key_value_heads,
                                       c.head_dim, c.intermediate_size, c.num_hidden_layers, c.max_length,
                                       c.rms_norm_eps, c.rope_theta), seed=0, wmode=wmode, kv_f16=kv_f16)
@@ -164,6 +163,8 @@ def _oneshot_rank(rank, world, port, name, batch, q, mode="oneshot", w="f16", pr
                        device=dev, seed=0, batch=batch).init()
         tp.open_oneshot(m)
         m.set_allreduce(mode)
+        if qa and m.fused_qkv_attn() != 1:
+            raise AssertionError("+qa: the q/k/v + attention launch was not taken at this shape")
         dist.barrier()
         if prefill:
             path = m.prefill_path()
@@ -260,12 +261,14 @@ def test_oneshot_prefill_two_processes(gpu, mode):
                                                ("tiny-gqa", 2, "fused", "i8"), ("tiny-h8", 4, "fused_wg", "f16"),
                                                ("tiny-gqa", 2, "fused_wg", "i8"), ("llama2-7b:2", 2, "fused_wg", "f16"),
                                                ("llama2-7b:2", 2, "fused", "f16"), ("tiny-h8", 4, "fused_wg+qa", "f16"),
-                                               ("tiny-gqa", 2, "fused+qa", "i8"), ("tiny-h8", 4, "fused+qa", "f16")])
+                                               ("tiny-gqa", 2, "fused+qa", "i8"), ("tiny-h8", 4, "fused+qa", "f16"),
+                                               ("llama2-7b:2", 4, "fused+qa", "f16")])
 def test_oneshot_allreduce_more_ranks(gpu, oracle, name, world, mode, w):
     """The one-shot exchange (separate launch or fused into wo / down) between 4 rank processes on one GPU, the
     fused forms with int8 weights, and both fused forms at Llama-2-7B shard shapes (2 layers, TP 2: 64 / 256
     workgroups per wo / down launch): tokens identical to the TP = 1 engine, logits within 1e-3, no device
-    error."""
+    error. "+qa": q/k/v + attention as one launch on every rank, also held directly to the oracle, at the tiny
+    shapes and at Llama-2-7B's TP-4 shards (2 layers, head_dim 128, 8 heads x 8 splits per rank)."""
     from simplellminference_amd.model import LlamaModel
     ref = LlamaModel(config=_preset(name), w_dtype=w, kv_dtype="f16", seed=0).init()
     rtoks, rlogits = ref.predict(PROMPT, 16, want_logits=True)
