@@ -292,7 +292,7 @@ def test_oneshot_allreduce_more_ranks(gpu, oracle, name, world, mode, w):
         assert np.abs(logits - ologits).max() <= 1e-3
 
 
-def _absent_peer_rank(rank, world, port, q):
+def _absent_peer_rank(rank, world, port, q, mode="fused"):
     """Rank 0 steps with the fused exchange while rank 1 never does: rank 0's first wait gives up after the bounded
     spin, every later one at once (oneshot.h os_gave_up)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0",
@@ -307,7 +307,7 @@ def _absent_peer_rank(rank, world, port, q):
     try:
         m = LlamaModel(config=preset("tiny"), w_dtype="f16", kv_dtype="f16", tp_rank=rank, tp_size=world, seed=0).init()
         tp.open_oneshot(m)
-        m.set_allreduce("fused")
+        m.set_allreduce(mode)
         dist.barrier()
         if rank == 0:
             def run(steps):  # steps x (2 layers x the wo / down exchanges + the argmax-key exchange)
@@ -333,7 +333,8 @@ def _absent_peer_rank(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_oneshot_absent_peer_gives_up_once(gpu):
+@pytest.mark.parametrize("mode", ["fused", "fused_wg"])
+def test_oneshot_absent_peer_gives_up_once(gpu, mode):
     """A peer that never arrives (rank 1 maps the buffers and does not step): rank 0's predict ends with
     DevState::error bit 4 after ONE bounded wait, not one per exchange (oneshot.h os_gave_up: later waits give up
     after 4096 polls): 3 steps take about as long as 1 (measured: 1 step, 5 exchanges, 2.57 s; 3 steps, 15 exchanges,
@@ -342,7 +343,7 @@ def test_oneshot_absent_peer_gives_up_once(gpu):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_absent_peer_rank, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_absent_peer_rank, args=(r, 2, port, q, mode)) for r in range(2)]
     for p in procs:
         p.start()
     status, times, msgs, refused = q.get(timeout=600)
@@ -351,6 +352,6 @@ def test_oneshot_absent_peer_gives_up_once(gpu):
     assert status == "ok", times
     assert all("one-shot all-reduce timed out" in msg for msg in msgs), msgs
     t1, t3 = times
-    print(f"absent peer: 1 step (5 exchanges) {t1:.2f} s, 3 steps (15 exchanges) {t3:.2f} s")
+    print(f"absent peer ({mode}): 1 step (5 exchanges) {t1:.2f} s, 3 steps (15 exchanges) {t3:.2f} s")
     assert t3 < 2.0 * t1  # one bounded wait each (3x that without the give-up)
     assert refused
