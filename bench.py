@@ -48,7 +48,8 @@ FAMILY_KERNELS = {
                        "sigmoid(g)*u)",
             "down": "gemv_kernel<EpiStoreSum> (down GEMV + residual + wo partials -> x)",
             "lm_head": "gemv_kernel<EpiLogits> (RMSNorm + tied LM head + argmax keys)"},
-    True: {"qkv": "bgemm_kernel<BgEpiQKV> (MFMA 16x16x32 f16)", "attention": "attn_partial_kernel (batched kv heads)",
+    True: {"qkv": "bgemm_kernel<BgEpiQKV> (MFMA 16x16x32 f16)", "attention": "attn_mfma_kernel (fp16 cache: LDS-DMA K/V, MFMA 16x16x32 f16, in-launch "
+                                                                    "split merge)",
            "wo": "bgemm_kernel<BgEpiStore> (MFMA)", "gate_up": "bgemm_kernel<BgEpiSwiGLU> (MFMA)",
            "down": "bgemm_kernel<BgEpiStore> (MFMA)", "lm_head": "bgemm_kernel<BgEpiLogits> (MFMA)"},
 }
@@ -71,6 +72,9 @@ def parse():
     ap.add_argument("--prefill-tokens", type=int, default=512,
                     help="after the decode timing: prefill a prompt of this many tokens (0: skip; batch 1 only)")
     ap.add_argument("--prefill-reps", type=int, default=3, help="timed prefill repetitions (after one warm-up)")
+    ap.add_argument("--settle-ms", type=float, default=1000.0,
+                    help="untimed warm-up before the --warmup steps: replay the step for this much wall time "
+                         "(0: one step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--greedy-steps", type=int, default=64, help="the greedy sanity run's length (profiling passes: 2)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample budget")
@@ -195,6 +199,59 @@ def _own_gpus(dist, torch, local: int, world: int) -> bool:
     return "?" not in key and len(set(keys)) == world
 
 
+class StepMarks:
+    """HIP events recorded on the engine stream between the timed loop's graph replays. Recording is an
+    enqueue (no host wait), so the timed loop keeps its host cadence; the durations are read after the
+    closing barrier."""
+
+    def __init__(self, torch, model, device, n):
+        self.stream = torch.cuda.ExternalStream(model.stream(), device=device)
+        self.ev = [torch.cuda.Event(enable_timing=True) for _ in range(n + 1)]
+
+    def start(self):
+        self.ev[0].record(self.stream)
+
+    def mark(self, i):
+        self.ev[i + 1].record(self.stream)
+
+    def durations_ms(self):
+        return [a.elapsed_time(b) for a, b in zip(self.ev[:-1], self.ev[1:])]
+
+
+def step_stats(ms: list, mean_ms: float) -> dict:
+    """p50 / p99 / min / max and the first-5 / last-5 means of the per-step device durations (HIP events),
+    beside the host-clock mean of the same window."""
+    import numpy as np
+    v = np.asarray(ms, np.float64)
+    k = min(5, len(v))
+    p50 = float(np.percentile(v, 50))
+    return {"source": "HIP events between consecutive graph replays on the engine stream (timed window)",
+            "n": int(len(v)), "p50": round(p50, 4), "p99": round(float(np.percentile(v, 99)), 4),
+            "min": round(float(v.min()), 4), "max": round(float(v.max()), 4), "mean": round(float(v.mean()), 4),
+            "first5_mean": round(float(v[:k].mean()), 4), "last5_mean": round(float(v[-k:].mean()), 4),
+            "host_clock_mean": round(mean_ms, 4),
+            "p50_over_host_mean": round(p50 / mean_ms, 4) if mean_ms > 0 else None}
+
+
+def settle_device(model, barrier, settle_ms: float, elapsed_max=lambda s: s) -> dict:
+    """Warm-up policy, before the --warmup steps: replay the step until the device has run it for settle_ms
+    of wall time (at least one step). A fresh box's first few milliseconds of replays run slower than its
+    steady state (clock and first-replay effects; round 5's driver window was 2.9 % behind its own greedy run
+    at --warmup 5), so a count-only warm-up of a few steps does not reach the state the window is meant to
+    time. Untimed, like --warmup; --steps and --warmup keep their meaning."""
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        model.step()
+        n += 1
+        if n % 8 == 0 or settle_ms <= 0:
+            barrier()
+            # every rank takes the same decision (the max over ranks), so all replay the same step count
+            if elapsed_max((time.perf_counter() - t0) * 1e3) >= settle_ms:
+                break
+    return {"steps": n, "ms": round((time.perf_counter() - t0) * 1e3, 1)}
+
+
 def progress(msg):
     """A progress line on stderr (long profiled runs stay visibly alive; stdout keeps the one JSON line)."""
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
@@ -281,12 +338,25 @@ def main():
                     model.set_state_seq(b, 1234 + 17 * b, a.ctx - 1, advance=False)
                 allreduce = "rccl (one-shot validation failed)"
     progress("model ready, timing the step")
+    def elapsed_max(v):
+        if not dist_on:
+            return v
+        t = torch.tensor([v], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    settle = settle_device(model, barrier, a.settle_ms, elapsed_max)
     for _ in range(a.warmup):
         model.step()
     barrier()
+    # one HIP event after every graph replay on the engine's own stream (no host sync inside the loop): the
+    # per-step device durations behind step_ms (SURVEY §5's p50 / p99; model.cpp:157-185 is the loop timed)
+    marks = StepMarks(torch, model, local, a.steps)
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    marks.start()
+    for i in range(a.steps):
         model.step()
+        marks.mark(i)
     barrier()
     elapsed = time.perf_counter() - t0
     if dist_on:
@@ -391,7 +461,10 @@ def main():
                                                   "frac": round(g["bytes_per_launch"] / (g["avg_us"] * 1e-6) / 1e9
                                                                 / HBM_PEAK_GBS, 4)}},
         "greedy_64": greedy,
+        "step_ms": step_stats(marks.durations_ms(), ms),
+        "settle": {**settle, "note": "untimed replays before the --warmup steps (--settle-ms)"},
     }
+    out["greedy_64"]["timed_mean_over_greedy"] = round(ms / greedy["ms_per_step"], 4)
     if B > 1:  # MFMA work of the batched projections: 2 flop per weight per sequence
         wb_el = {"f16": 2.0, "i8": 1.0, "f32": 4.0}[a.w_dtype]
         proj = [f for f in fam if f != "attention"]
@@ -461,5 +534,18 @@ def main():
         dist.destroy_process_group()
 
 
+def _comm_fatal(e: BaseException) -> bool:
+    """An RCCL error or an expired bounded wait on this rank (sli.h SLI_ERR_COMM / SLI_ERR_TIMEOUT): the engine has
+    already aborted its communicator, so the rank ends here with a non-zero status — no retry, no re-exec."""
+    from simplellminference_amd._lib import SLI_ERR_COMM, SLI_ERR_TIMEOUT, SliError
+    return isinstance(e, SliError) and e.code in (SLI_ERR_COMM, SLI_ERR_TIMEOUT)
+
+
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except Exception as e:  # noqa: BLE001 - a wedged communicator must not leave the rank (or the node run) hanging
+        if not _comm_fatal(e):
+            raise
+        print(f"[bench] rank {os.environ.get('RANK', '0')}: {e}; exiting", file=sys.stderr, flush=True)
+        os._exit(3)  # skip interpreter teardown: destructors of a torch/RCCL stack behind a dead peer can block

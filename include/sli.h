@@ -31,7 +31,9 @@ typedef enum {
     SLI_ERR_HIP = 4,    /* HIP runtime error */
     SLI_ERR_NOMEM = 5,  /* device allocation failed */
     SLI_ERR_COMM = 6,   /* RCCL error */
-    SLI_ERR_STATE = 7   /* call not valid in the object's current state */
+    SLI_ERR_STATE = 7,  /* call not valid in the object's current state */
+    SLI_ERR_TIMEOUT = 8 /* a host wait on a stream with RCCL collectives made no progress for SLI_COMM_TIMEOUT_MS
+                           (default 120 s): a peer or the communicator is wedged; the communicator was aborted */
 } sli_status;
 
 typedef enum { SLI_DT_F32 = 0, SLI_DT_F16 = 1, SLI_DT_I8 = 2 } sli_dtype;
@@ -207,8 +209,8 @@ int sli_model_prefill(sli_model* m, const int32_t* ids, int32_t n);
 int sli_model_prefill_path(const sli_model* m);
 /* 1: the batch-1 decode step runs each layer's q/k/v projection and attention as ONE launch (qkv_attn.h: the
  * attention's K/V rows below the position stream while the projection runs; q and this step's K/V row are
- * handed over inside the launch); 2: the wo projection joins that launch too (SLI_QKV_CHAIN=1, opt-in, measured
- * slower); 0: separate launches (model.cpp:70-84's matmul / rope / mha sequence either way).
+ * handed over inside the launch); 0: separate launches (model.cpp:70-84's matmul / rope / mha sequence either
+ * way).
  * Taken where the shape qualifies (heads per kv head 1 or 2, head_dim 64 / 128, fp16 K/V cache, fp16 / int8
  * weights, an attention grid of at most a quarter of the CUs) and SLI_QKV_ATTN allows it
  * (1: always; 0: never; unset: single-rank models). */
@@ -227,6 +229,11 @@ int sli_model_set_exec(sli_model* m, int32_t mode);
 int sli_model_get_exec(sli_model* m, int32_t* mode);
 /* One decode step (hipGraph replay; captured on first use). Asynchronous on the model's stream. */
 int sli_model_step(sli_model* m);
+/* Host waits (sync, logits / state / history reads, predict, prefill, the timing probes) of a rank whose step
+ * carries RCCL collectives are bounded (csrc/comm_wait.h): they poll the stream, ncclCommGetAsyncError and a
+ * deadline; a communicator error returns SLI_ERR_COMM, an expired deadline SLI_ERR_TIMEOUT, and either aborts the
+ * communicator (ncclCommAbort), after which every call that would step returns SLI_ERR_COMM. The reference's
+ * all-reduce-free equivalents: the logits copy at model.cpp:175-179. */
 int sli_model_sync(sli_model* m);
 /* logits of the last step: this rank's vocab shard [vocab_lo, vocab_lo+n) of every sequence, [batch][n]. */
 int sli_model_get_logits(sli_model* m, float* host, int32_t n, int32_t* vocab_lo);
@@ -294,6 +301,11 @@ int sli_model_time_families(sli_model* m, int32_t iters, double* us, double* byt
  * allocated context), replayed the same way; us[f] = mean device µs per launch (the
  * fraction of a measured stream-copy bandwidth). */
 int sli_model_time_stream(sli_model* m, int32_t iters, double* us);
+/* Test hook (no device needed): runs the bounded-wait policy of comm_wait.h against mocked probes. mode 0: a
+ * query that completes on its 3rd poll (SLI_OK); 1: a query that never completes (SLI_ERR_TIMEOUT after
+ * deadline_ms); 2: an async communicator error on the 2nd poll (SLI_ERR_COMM); 3: a failing query (SLI_ERR_HIP).
+ * *waited_ms = the wall time the wait took. */
+int sli_debug_bounded_wait(int32_t mode, double deadline_ms, double* waited_ms);
 
 #ifdef __cplusplus
 }

@@ -16,7 +16,8 @@ from dataclasses import dataclass
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+# SLI_ORACLE_LIB: an alternative build of the same source (tools/asan_check.sh: the ASan/UBSan build, _ref/asan/)
+_LIB_PATH = os.environ.get("SLI_ORACLE_LIB") or os.path.join(_HERE, "liboracle.so")
 _lib = None
 
 F32P = ctypes.POINTER(ctypes.c_float)
@@ -29,6 +30,8 @@ W_F32, W_F16, W_I8 = 0, 1, 2
 
 def build(force: bool = False) -> str:
     """Compile liboracle.so with the committed Makefile (gcc)."""
+    if os.environ.get("SLI_ORACLE_LIB"):
+        return _LIB_PATH
     if force or not os.path.exists(_LIB_PATH):
         subprocess.run(["make", "-s", "-C", _HERE] + (["-B"] if force else []), check=True)
     return _LIB_PATH

@@ -18,7 +18,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 REF_ROOT = os.environ.get("SLI_REFERENCE", "/root/reference")
-LIB_PATH = os.path.join(_HERE, "_ref", "libref.so")
+LIB_PATH = os.environ.get("SLI_REF_LIB") or os.path.join(_HERE, "_ref", "libref.so")  # (asan_check.sh: _ref/asan/)
 _lib = None
 
 F32P = ctypes.POINTER(ctypes.c_float)

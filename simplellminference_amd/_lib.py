@@ -14,7 +14,8 @@ LIB_PATH = os.path.join(_HERE, "libsli.so" if not os.environ.get("SLI_LIB_VARIAN
 
 SLI_OK = 0
 STATUS = {0: "ok", 1: "invalid argument", 2: "shape mismatch", 3: "index out of range", 4: "HIP runtime error",
-          5: "out of device memory", 6: "RCCL error", 7: "invalid state"}
+          5: "out of device memory", 6: "RCCL error", 7: "invalid state", 8: "communicator wait timed out"}
+SLI_ERR_COMM, SLI_ERR_TIMEOUT = 6, 8
 DT_F32, DT_F16, DT_I8 = 0, 1, 2
 
 c_int, c_i32, c_u32, c_i64, c_f, c_d, c_vp, c_sz = (ctypes.c_int, ctypes.c_int32, ctypes.c_uint32, ctypes.c_int64,
@@ -112,6 +113,7 @@ _SIGS = {
     "sli_model_time_steps": (c_int, [c_vp, c_i32, P_d]),
     "sli_model_time_families": (c_int, [c_vp, c_i32, P_d, P_d, P_i32]),
     "sli_model_time_stream": (c_int, [c_vp, c_i32, P_d]),
+    "sli_debug_bounded_wait": (c_int, [c_i32, c_d, P_d]),
     "sli_tp_group_create": (c_int, [ctypes.POINTER(ModelConfig), c_i32, ctypes.POINTER(c_vp)]),
     "sli_tp_group_destroy": (c_int, [c_vp]),
     "sli_tp_group_rank": (c_int, [c_vp, c_i32, ctypes.POINTER(c_vp)]),

@@ -26,6 +26,7 @@
 #include "../../include/sli_synth.h"
 #include "attention.h"
 #include "bgemm.h"
+#include "comm_wait.h"
 #include "common.h"
 #include "gemv.h"
 #include "oneshot.h"
@@ -115,6 +116,7 @@ struct sli_model {
     char* os_peer[sli::kOsMaxRanks] = {};    // every rank's buffer mapped here (own included)
     bool os_open = false;
     bool os_dead = false;                    // a one-shot wait timed out: set_allreduce(ONESHOT) is refused
+    bool comm_dead = false;                  // a bounded host wait aborted the RCCL communicator (comm_wait.h)
     unsigned* os_epoch = nullptr;            // one-shot call counter; os_epoch[1..9]: fused-launch arrivals
     unsigned* os_wg_epoch = nullptr;         // per-(region, workgroup) epochs [kOsRegions][kOsMaxWg] (oneshot.h)
     int os_nmax = 0;
@@ -1124,6 +1126,7 @@ static int bg_sync_tiles(sli_model* m) {
 }
 
 static int capture(sli_model* m) {
+    if (m->comm_dead) return fail(SLI_ERR_COMM, "the RCCL communicator was aborted by an earlier bounded wait");
     SLI_TRY(bg_sync_tiles(m));
     return capture_graph(m->stream, m->graph, m->graph_exec, [&]() { return SLI_DISPATCH(m, record, m); });
 }
@@ -1136,16 +1139,65 @@ static int capture_group(sli_tp_group* g) {
     return capture_graph(g->stream, g->graph, g->exec, [&]() { return SLI_DISPATCH(m0, record_group, g); });
 }
 
+// ---- bounded host waits (comm_wait.h): a rank whose step holds RCCL collectives never blocks in
+// hipStreamSynchronize on a wedged peer; it polls the stream / event, ncclCommGetAsyncError and a deadline, and on
+// failure aborts the communicator (its kernels and proxy threads end) and reports which rank gave up and why.
+static int comm_abort(sli_model* m, int code, const std::string& why) {
+    if (m->comm) (void)ncclCommAbort(m->comm);
+    m->comm = nullptr;
+    m->comm_dead = true;
+    return fail(code, "tp rank " + std::to_string(m->c.tp_rank) + "/" + std::to_string(m->c.tp_size) + ": " + why);
+}
+template <class Query>
+static int wait_bounded(sli_model* m, Query query) {
+    std::string why;
+    const int rc = bounded_wait(
+        [&] {
+            const hipError_t e = query();
+            return e == hipSuccess ? WaitPoll::Done : e == hipErrorNotReady ? WaitPoll::Pending : WaitPoll::Failed;
+        },
+        [&](std::string& msg) {
+            ncclResult_t r = ncclSuccess;
+            if (ncclCommGetAsyncError(m->comm, &r) != ncclSuccess) {
+                msg = "ncclCommGetAsyncError failed";
+                return true;
+            }
+            if (r == ncclSuccess || r == ncclInProgress) return false;
+            msg = ncclGetErrorString(r);
+            return true;
+        },
+        steady_ms, comm_timeout_ms(), why);
+    if (rc == SLI_OK) return SLI_OK;
+    if (rc == SLI_ERR_HIP) return hip_fail(query(), why.c_str());
+    return comm_abort(m, rc, why);
+}
+static int wait_stream(sli_model* m) {
+    if (m->comm_dead) return fail(SLI_ERR_COMM, "the RCCL communicator was aborted by an earlier bounded wait");
+    if (!m->comm) {
+        SLI_HIP(hipStreamSynchronize(m->stream));
+        return SLI_OK;
+    }
+    return wait_bounded(m, [&] { return hipStreamQuery(m->stream); });
+}
+static int wait_event(sli_model* m, hipEvent_t e) {
+    if (m->comm_dead) return fail(SLI_ERR_COMM, "the RCCL communicator was aborted by an earlier bounded wait");
+    if (!m->comm) {
+        SLI_HIP(hipEventSynchronize(e));
+        return SLI_OK;
+    }
+    return wait_bounded(m, [&] { return hipEventQuery(e); });
+}
+
 static int upload_states(sli_model* m, const std::vector<DevState>& h) {
     SLI_HIP(hipMemcpyAsync(m->st, h.data(), sizeof(DevState) * m->B, hipMemcpyHostToDevice, m->stream));
-    SLI_HIP(hipStreamSynchronize(m->stream));
+    SLI_TRY(wait_stream(m));
     return SLI_OK;
 }
 
 static int download_states(sli_model* m, std::vector<DevState>& h) {
     h.resize(m->B);
     SLI_HIP(hipMemcpyAsync(h.data(), m->st, sizeof(DevState) * m->B, hipMemcpyDeviceToHost, m->stream));
-    SLI_HIP(hipStreamSynchronize(m->stream));
+    SLI_TRY(wait_stream(m));
     return SLI_OK;
 }
 
@@ -1175,6 +1227,12 @@ static int check_device_errors(sli_model* m) {
 static void destroy(sli_model* m) {
     if (!m) return;
     (void)hipSetDevice(m->c.device);
+    if (m->comm_dead) {
+        // an aborted communicator: work may still sit on the stream behind a wedged peer, so nothing is freed (the
+        // process is about to exit on that error; freeing under running kernels would be worse than the leak)
+        delete m;
+        return;
+    }
     if (m->stream) (void)hipStreamSynchronize(m->stream);
     if (m->graph_exec) (void)hipGraphExecDestroy(m->graph_exec);
     if (m->graph) (void)hipGraphDestroy(m->graph);
@@ -1464,7 +1522,7 @@ int sli_model_init_synthetic(sli_model* m, uint32_t seed) {
     const int kinds[] = {SLI_T_WQ, SLI_T_WK, SLI_T_WV, SLI_T_WO, SLI_T_UP, SLI_T_GATE, SLI_T_DOWN};
     for (int l = 0; l < m->L; ++l)
         for (int k : kinds) SLI_TRY(place_tensor(m, k, l, src(k, l)));
-    SLI_HIP(hipStreamSynchronize(m->stream));
+    SLI_TRY(wait_stream(m));
     return SLI_OK;
 }
 
@@ -1480,7 +1538,7 @@ int sli_model_set_weight(sli_model* m, int32_t kind, int32_t index, const float*
     if (hipMemcpy(tmp, host, sizeof(float) * (size_t)n, hipMemcpyHostToDevice) != hipSuccess)
         rc = fail(SLI_ERR_HIP, "hipMemcpy weight");
     if (rc == SLI_OK) rc = place_tensor(m, kind, index, SrcBuf{tmp});
-    if (hipStreamSynchronize(m->stream) != hipSuccess && rc == SLI_OK) rc = fail(SLI_ERR_HIP, "sync");
+    if (rc == SLI_OK) rc = wait_stream(m);
     (void)hipFree(tmp);
     return rc;
 }
@@ -1535,7 +1593,7 @@ int sli_model_fill_kv_synthetic(sli_model* m, uint32_t seed, int32_t upto) {
     if (upto == 0) return SLI_OK;
     SLI_HIP(hipSetDevice(m->c.device));
     SLI_TRY(SLI_DISPATCH(m, fill_kv, m, seed, upto));
-    SLI_HIP(hipStreamSynchronize(m->stream));
+    SLI_TRY(wait_stream(m));
     return SLI_OK;
 }
 
@@ -1564,6 +1622,7 @@ static int set_prompt(sli_model* m, int seq, const int32_t* ids, int32_t n) {
     SLI_CHECK(m && ids, SLI_ERR_ARG, "null argument");
     SLI_CHECK(seq < m->B, SLI_ERR_RANGE, "sequence index out of range");
     SLI_CHECK(n >= 1 && n <= m->T, SLI_ERR_RANGE, "prompt length out of range");
+    SLI_CHECK(!m->comm_dead, SLI_ERR_COMM, "the RCCL communicator was aborted by an earlier bounded wait");
     for (int i = 0; i < n; ++i)
         SLI_CHECK(ids[i] >= 0 && ids[i] < m->V, SLI_ERR_RANGE, "Token index is greater than vocab size.");
     std::vector<DevState> h;
@@ -1669,7 +1728,7 @@ extern "C" int sli_model_prefill(sli_model* m, const int32_t* ids, int32_t n) {
             SLI_HIP(hipMemcpyAsync(m->pf.ps, &c, sizeof(PfState), hipMemcpyHostToDevice, m->stream));
             SLI_HIP(hipGraphLaunch(m->pf.exec[pf_bucket(c.nv)], m->stream));
         }
-        SLI_HIP(hipStreamSynchronize(m->stream));
+        SLI_TRY(wait_stream(m));
     } else {
         for (int p = 0; p < n - 1; ++p) {  // the decode step, teacher-forced (model.cpp:159-165)
             SLI_TRY(set_state(m, 0, ids[p], p, 0));
@@ -1727,7 +1786,7 @@ extern "C" int sli_model_predict_prefill(sli_model* m, const int32_t* prompt, in
         if (logits_out) SLI_TRY(sli_model_get_logits(m, logits_out + (size_t)t * per_step, (int32_t)per_step, nullptr));
     }
     SLI_HIP(hipMemcpyAsync(tokens_out, m->hist, sizeof(int32_t) * max_length, hipMemcpyDeviceToHost, m->stream));
-    SLI_HIP(hipStreamSynchronize(m->stream));
+    SLI_TRY(wait_stream(m));
     return check_device_errors(m);
 }
 
@@ -1763,7 +1822,7 @@ int sli_model_get_history(sli_model* m, int32_t seq, int32_t n, int32_t* out) {
     SLI_CHECK(seq >= 0 && seq < m->B && n >= 0 && n <= m->T, SLI_ERR_RANGE, "sequence / length out of range");
     SLI_HIP(hipMemcpyAsync(out, m->hist + (size_t)seq * (m->T + 1), sizeof(int32_t) * n, hipMemcpyDeviceToHost,
                            m->stream));
-    SLI_HIP(hipStreamSynchronize(m->stream));
+    SLI_TRY(wait_stream(m));
     return SLI_OK;
 }
 
@@ -1773,7 +1832,7 @@ int sli_model_set_exec(sli_model* m, int32_t mode) {
               "unknown execution mode (the persistent one-launch step was removed in round 5: DESIGN.md §9)");
     SLI_HIP(hipSetDevice(m->c.device));
     if (mode != m->exec) {  // re-capture the step graph on the next step
-        SLI_HIP(hipStreamSynchronize(m->stream));
+        SLI_TRY(wait_stream(m));
         if (m->graph_exec) (void)hipGraphExecDestroy(m->graph_exec);
         if (m->graph) (void)hipGraphDestroy(m->graph);
         m->graph_exec = nullptr;
@@ -1799,7 +1858,7 @@ int sli_model_step(sli_model* m) {
 
 int sli_model_sync(sli_model* m) {
     SLI_CHECK(m, SLI_ERR_ARG, "null model");
-    SLI_HIP(hipStreamSynchronize(m->stream));
+    SLI_TRY(wait_stream(m));
     return SLI_OK;
 }
 
@@ -1807,7 +1866,7 @@ int sli_model_get_logits(sli_model* m, float* host, int32_t n, int32_t* vocab_lo
     SLI_CHECK(m && host, SLI_ERR_ARG, "null argument");
     SLI_CHECK(n >= m->B * m->v_n, SLI_ERR_SHAPE, "host buffer smaller than the local vocab shard x batch");
     SLI_HIP(hipMemcpyAsync(host, m->logits, sizeof(float) * m->B * m->v_n, hipMemcpyDeviceToHost, m->stream));
-    SLI_HIP(hipStreamSynchronize(m->stream));
+    SLI_TRY(wait_stream(m));
     if (vocab_lo) *vocab_lo = m->v_lo;
     return SLI_OK;
 }
@@ -1829,7 +1888,7 @@ int sli_model_predict_batch(sli_model* m, const int32_t* prompts, const int32_t*
     for (int b = 0; b < m->B; ++b)
         SLI_HIP(hipMemcpyAsync(tokens_out + (size_t)b * max_length, m->hist + (size_t)b * (m->T + 1),
                                sizeof(int32_t) * max_length, hipMemcpyDeviceToHost, m->stream));
-    SLI_HIP(hipStreamSynchronize(m->stream));
+    SLI_TRY(wait_stream(m));
     return check_device_errors(m);
 }
 
@@ -1857,7 +1916,7 @@ int sli_model_get_kv_seq(sli_model* m, int32_t seq, int32_t layer, int32_t which
     int rc = SLI_DISPATCH(m, get_kv, m, seq, layer, which, upto, tmp);
     if (rc == SLI_OK && hipMemcpyAsync(host, tmp, n * 4, hipMemcpyDeviceToHost, m->stream) != hipSuccess)
         rc = fail(SLI_ERR_HIP, "copy kv");
-    if (hipStreamSynchronize(m->stream) != hipSuccess && rc == SLI_OK) rc = fail(SLI_ERR_HIP, "sync");
+    if (rc == SLI_OK) rc = wait_stream(m);
     (void)hipFree(tmp);
     return rc;
 }
@@ -2016,7 +2075,7 @@ int sli_model_set_allreduce(sli_model* m, int32_t mode) {
     SLI_CHECK(mode == SLI_ALLREDUCE_RCCL || m->exec == SLI_EXEC_LAUNCHES, SLI_ERR_STATE,
               "tensor parallelism runs the launch graph");
     if (mode != m->ar_mode) {
-        SLI_HIP(hipStreamSynchronize(m->stream));
+        SLI_TRY(wait_stream(m));
         if (m->graph_exec) (void)hipGraphExecDestroy(m->graph_exec);
         if (m->graph) (void)hipGraphDestroy(m->graph);
         m->graph_exec = nullptr;
@@ -2024,6 +2083,27 @@ int sli_model_set_allreduce(sli_model* m, int32_t mode) {
         m->ar_mode = mode;
     }
     return SLI_OK;
+}
+
+int sli_debug_bounded_wait(int32_t mode, double deadline_ms, double* waited_ms) {
+    SLI_CHECK(mode >= 0 && mode <= 3 && deadline_ms >= 0.0 && waited_ms, SLI_ERR_ARG, "bad argument");
+    int polls = 0;
+    std::string why;
+    const double t0 = steady_ms();
+    const int rc = bounded_wait(
+        [&] {
+            ++polls;
+            if (mode == 3) return WaitPoll::Failed;
+            return mode == 0 && polls >= 3 ? WaitPoll::Done : WaitPoll::Pending;
+        },
+        [&](std::string& msg) {
+            if (mode != 2 || polls < 2) return false;
+            msg = "mocked remote error";
+            return true;
+        },
+        steady_ms, deadline_ms, why);
+    *waited_ms = steady_ms() - t0;
+    return rc == SLI_OK ? SLI_OK : fail(rc, why);
 }
 
 int sli_model_time_steps(sli_model* m, int32_t iters, double* avg_us) {
@@ -2043,7 +2123,7 @@ int sli_model_time_steps(sli_model* m, int32_t iters, double* avg_us) {
     SLI_HIP(hipEventRecord(g.e0, m->stream));
     for (int i = 0; i < iters; ++i) SLI_HIP(hipGraphLaunch(m->graph_exec, m->stream));
     SLI_HIP(hipEventRecord(g.e1, m->stream));
-    SLI_HIP(hipEventSynchronize(g.e1));
+    SLI_TRY(wait_event(m, g.e1));
     float ms = 0.0f;
     SLI_HIP(hipEventElapsedTime(&ms, g.e0, g.e1));
     *avg_us = 1000.0 * ms / iters;
@@ -2092,13 +2172,14 @@ int sli_model_time_families(sli_model* m, int32_t iters, double* us, double* byt
         if (rc == SLI_OK && hipEventRecord(g.e1, m->stream) != hipSuccess) rc = fail(SLI_ERR_HIP, "event");
         float ms = 0.0f;
         if (rc == SLI_OK &&
-            (hipEventSynchronize(g.e1) != hipSuccess || hipEventElapsedTime(&ms, g.e0, g.e1) != hipSuccess))
+            (rc = wait_event(m, g.e1)) == SLI_OK && hipEventElapsedTime(&ms, g.e0, g.e1) != hipSuccess)
             rc = fail(SLI_ERR_HIP, "event timing");
         us[f] = 1000.0 * ms / ((double)iters * launches[f]);
     }
-    if (hipMemcpyAsync(m->x, g.xsave, xb, hipMemcpyDeviceToDevice, m->stream) != hipSuccess ||
-        hipStreamSynchronize(m->stream) != hipSuccess) {
+    if (hipMemcpyAsync(m->x, g.xsave, xb, hipMemcpyDeviceToDevice, m->stream) != hipSuccess) {
         if (rc == SLI_OK) rc = fail(SLI_ERR_HIP, "restore x");
+    } else if (rc == SLI_OK) {
+        rc = wait_stream(m);
     }
     return rc;
 }
@@ -2173,7 +2254,7 @@ int sli_model_time_stream(sli_model* m, int32_t iters, double* us) {
         SLI_HIP(hipEventRecord(g.e1, m->stream));
         SLI_HIP(hipGetLastError());
         float ms = 0.0f;
-        SLI_HIP(hipEventSynchronize(g.e1));
+        SLI_TRY(wait_event(m, g.e1));
         SLI_HIP(hipEventElapsedTime(&ms, g.e0, g.e1));
         us[f] = 1000.0 * ms / ((double)iters * n);
     }
@@ -2207,11 +2288,12 @@ int sli_model_time_gemv(sli_model* m, int32_t iters, double* avg_us, double* byt
     for (int i = 0; rc == SLI_OK && i < iters; ++i) rc = SLI_DISPATCH(m, gemvs, m);
     if (rc == SLI_OK) rc = hipEventRecord(g.e1, m->stream) == hipSuccess ? SLI_OK : fail(SLI_ERR_HIP, "event");
     float ms = 0.0f;
-    if (rc == SLI_OK && (hipEventSynchronize(g.e1) != hipSuccess || hipEventElapsedTime(&ms, g.e0, g.e1) != hipSuccess))
+    if (rc == SLI_OK && (rc = wait_event(m, g.e1)) == SLI_OK && hipEventElapsedTime(&ms, g.e0, g.e1) != hipSuccess)
         rc = fail(SLI_ERR_HIP, "event timing");
-    if (hipMemcpyAsync(m->x, g.xsave, xb, hipMemcpyDeviceToDevice, m->stream) != hipSuccess ||
-        hipStreamSynchronize(m->stream) != hipSuccess) {
+    if (hipMemcpyAsync(m->x, g.xsave, xb, hipMemcpyDeviceToDevice, m->stream) != hipSuccess) {
         if (rc == SLI_OK) rc = fail(SLI_ERR_HIP, "restore x");
+    } else if (rc == SLI_OK) {
+        rc = wait_stream(m);
     }
     if (rc != SLI_OK) return rc;
     const int n_launch = 4 * m->L + 1;

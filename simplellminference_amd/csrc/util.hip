@@ -50,6 +50,7 @@ const char* sli_status_str(int status) {
         case SLI_ERR_NOMEM: return "out of device memory";
         case SLI_ERR_COMM: return "RCCL error";
         case SLI_ERR_STATE: return "invalid state";
+        case SLI_ERR_TIMEOUT: return "communicator wait timed out";
         default: return "unknown status";
     }
 }

@@ -167,8 +167,9 @@ class LlamaModel:
     EXEC = {"launches": 0}
 
     def set_exec(self, mode: str) -> "LlamaModel":
-        """"launches": one graph of fused launches (the only mode since round 5)."""
-        call("sli_model_set_exec", self._h, self.EXEC[mode])
+        """"launches": one graph of fused launches (the only mode since round 5). Any other name (e.g. the removed
+        "persistent") goes to the C layer as an unknown mode, which raises SliError(SLI_ERR_ARG) with its message."""
+        call("sli_model_set_exec", self._h, self.EXEC.get(mode, -1))
         return self
 
     def exec_mode(self) -> str:
