@@ -221,10 +221,15 @@ int sli_model_predict_prefill(sli_model* m, const int32_t* prompt, int32_t n_pro
                               int32_t* tokens_out, float* logits_out);
 /* The tokens fed at positions [0, n) of sequence seq. */
 int sli_model_get_history(sli_model* m, int32_t seq, int32_t n, int32_t* out);
-/* Execution of the step: SLI_EXEC_LAUNCHES, one hipGraph of ~5 fused launches per layer (every configuration).
- * (Round 5 removed the opt-in persistent one-launch step, mode 1: measured slower every round, DESIGN.md §9;
- * sli_model_set_exec(1) returns SLI_ERR_ARG.) */
-enum { SLI_EXEC_LAUNCHES = 0 };
+/* Execution of the step: SLI_EXEC_LAUNCHES, one hipGraph of ~5 fused launches per layer (every configuration);
+ * SLI_EXEC_PERSIST, the embedding, then EVERY layer as one persistent launch (csrc/tp_layers.h: one workgroup per
+ * CU, each op's weight share in registers before its input arrives, the edges as tagged granules, the residual
+ * exchange per workgroup inside the launch), then the LM head launches. Taken for batch-1 fp16 models at head_dim
+ * 128 whose per-workgroup shares fit (the TP-4 / TP-8 shards of Llama-2-7B); otherwise SLI_ERR_STATE with the
+ * reason. Under tensor parallelism it needs the one-shot buffers and SLI_ALLREDUCE_FUSED_WG (ranks on distinct
+ * devices), or no communicator (SLI_DEBUG_NOCOMM). Not for the ranks of an in-process group.
+ * (Round 5 removed the opt-in persistent one-launch step, mode 1; sli_model_set_exec(1) returns SLI_ERR_ARG.) */
+enum { SLI_EXEC_LAUNCHES = 0, SLI_EXEC_PERSIST = 2 };
 int sli_model_set_exec(sli_model* m, int32_t mode);
 int sli_model_get_exec(sli_model* m, int32_t* mode);
 /* One decode step (hipGraph replay; captured on first use). Asynchronous on the model's stream. */

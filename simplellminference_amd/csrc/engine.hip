@@ -35,6 +35,7 @@
 #include "qkv_attn.h"
 #include "rope_table.h"
 #include "step_state.h"
+#include "tp_layers.h"
 
 namespace sli {
 
@@ -124,6 +125,15 @@ struct sli_model {
     char** os_peer_tab = nullptr;            // device copy of os_peer (oneshot.h EpiPush::peer_tab)
     size_t os_bytes = 0;
     int exec = SLI_EXEC_LAUNCHES;
+    // SLI_EXEC_PERSIST: the layer stack as one persistent launch (tp_layers.h); its granule arrays, weight table,
+    // launch counter and the device table of every rank's exchange granules (in the one-shot comm buffers)
+    struct Tl {
+        sli::tl_u2 *g_x = nullptr, *g_qkv = nullptr, *g_part = nullptr, *g_att = nullptr, *g_x1 = nullptr,
+                   *g_act = nullptr;
+        const __half** w = nullptr;
+        unsigned* epoch = nullptr;
+        sli::tl_u2** xg = nullptr;
+    } tl;
 };
 
 // In-process tensor parallelism (the "fake communicator"): tp_size rank models on
@@ -454,6 +464,129 @@ static bool qkv_attn_on(const sli_model* m) {
 // round: profiles/r4_c4_merge_launch_ab.txt); the MFMA attention (fp16 cache) merges inside its one resident
 // round (ops.hip attn_mfma_launch).
 constexpr int kDeferBatched = 2;
+
+// ---------------------------------------------------------------- the layer stack as one persistent launch
+// (SLI_EXEC_PERSIST, tp_layers.h). Taken for batch-1 fp16 models at head_dim 128 whose per-workgroup shares fit the
+// kernel's LDS partial buffer: the TP-4 / TP-8 shards of Llama-2-7B (C2), not the unsharded 7B.
+static int tpl_nwg() { return gemv_max_blocks(); }
+
+static int tpl_check(const sli_model* m, std::string* why) {
+    auto no = [&](const char* r) {
+        if (why) *why = r;
+        return 0;
+    };
+    if (m->group) return no("the ranks of an in-process group step in lockstep launches (their exchange is between launches)");
+    if (m->B != 1) return no("batch 1 only");
+    if (m->c.w_dtype != SLI_DT_F16 || m->c.kv_dtype != SLI_DT_F16) return no("fp16 weights and K/V cache only");
+    if (m->hd != kTlHD) return no("head_dim 128 only");
+    const int G = m->hq / m->hkv;
+    if (!(G == 1 || G == 2 || G == 4)) return no("1, 2 or 4 query heads per kv head");
+    if (m->D % 8 || m->Il % 8 || m->D > kTlMaxX || m->Il > kTlMaxX || m->hq * kTlHD > kTlMaxX)
+        return no("D and the local FFN width must be multiples of 8 and at most 8192");
+    if ((m->T + kTlKS - 1) / kTlKS > kTlMaxSplits) return no("context at most 8192");
+    const int nwg = tpl_nwg();
+    auto cdiv = [](long long a, long long b) { return (int)((a + b - 1) / b); };
+    const int nrow = cdiv(m->D, nwg), nq = cdiv((long long)(m->hq + 2 * m->hkv) * (kTlHD / 2), nwg),
+              ng = cdiv(m->Il, nwg);
+    if (nrow > kTlMaxRows) return no("too many residual rows per workgroup");
+    const long long need[] = {2LL * nq * (m->D / 8), (long long)nrow * m->hq * kTlHD / 8, 2LL * ng * (m->D / 8),
+                              (long long)nrow * (m->Il / 8), (long long)kOsMaxRanks * nrow};
+    for (long long n : need)
+        if (n > kTlPartMax) return no("the per-workgroup shares exceed the kernel's LDS partial buffer (an unsharded 7B)");
+    if (m->partial) {
+        const bool wg = m->ar_mode == SLI_ALLREDUCE_FUSED_WG && m->os_open;
+        const bool nocomm = !m->collectives && !m->os_open;
+        if (!wg && !nocomm)
+            return no("under tensor parallelism the exchange runs inside the launch: set_allreduce(fused_wg) first");
+    }
+    return 1;
+}
+
+static int tpl_alloc(sli_model* m) {
+    if (m->tl.w) return SLI_OK;
+    const int S = (m->T + kTlKS - 1) / kTlKS;
+    const size_t n[6] = {(size_t)m->D, (size_t)(m->hq + 2 * m->hkv) * kTlHD, (size_t)m->hq * S * kTlPart,
+                         (size_t)m->hq * kTlHD, (size_t)m->D, (size_t)m->Il};
+    tl_u2** dst[6] = {&m->tl.g_x, &m->tl.g_qkv, &m->tl.g_part, &m->tl.g_att, &m->tl.g_x1, &m->tl.g_act};
+    for (int i = 0; i < 6; ++i) {
+        SLI_TRY(model_alloc(m, (void**)dst[i], 8 * n[i]));
+        SLI_HIP(hipMemset(*dst[i], 0, 8 * n[i]));  // tag 0: never a launch's (epochs start at 1)
+    }
+    SLI_TRY(model_alloc(m, (void**)&m->tl.epoch, 16));
+    SLI_HIP(hipMemset(m->tl.epoch, 0, 16));
+    SLI_TRY(model_alloc(m, (void**)&m->tl.xg, sizeof(tl_u2*) * kOsMaxRanks));
+    std::vector<const __half*> w(4 * (size_t)m->L);
+    for (int l = 0; l < m->L; ++l) {
+        w[4 * l + 0] = (const __half*)m->layers[l].qkv;
+        w[4 * l + 1] = (const __half*)m->layers[l].wo;
+        w[4 * l + 2] = (const __half*)m->layers[l].gu;
+        w[4 * l + 3] = (const __half*)m->layers[l].down;
+    }
+    const __half** wd = nullptr;
+    SLI_TRY(model_alloc(m, (void**)&wd, sizeof(void*) * w.size()));
+    SLI_HIP(hipMemcpy(wd, w.data(), sizeof(void*) * w.size(), hipMemcpyHostToDevice));
+    m->tl.w = wd;
+    return SLI_OK;
+}
+
+// before a capture (no allocation or copy may run while the stream captures): buffers, and the device table of the
+// ranks' exchange granules as currently mapped
+static int tpl_prepare(sli_model* m) {
+    std::string why;
+    if (!tpl_check(m, &why)) return fail(SLI_ERR_STATE, "persistent layers: " + why);
+    SLI_TRY(tpl_alloc(m));
+    if (m->partial && m->os_open) {
+        tl_u2* xg[kOsMaxRanks] = {};
+        for (int r = 0; r < m->c.tp_size; ++r) xg[r] = (tl_u2*)(m->os_peer[r] + os_gran_off(m->os_nmax));
+        SLI_HIP(hipMemcpy(m->tl.xg, xg, sizeof(xg), hipMemcpyHostToDevice));
+    }
+    return SLI_OK;
+}
+
+static int tpl_launch(sli_model* m) {
+    std::string why;
+    if (!tpl_check(m, &why) || !m->tl.w) return fail(SLI_ERR_STATE, "persistent layers: " + why);
+    TlArgs a{};
+    a.D = m->D;
+    a.hq = m->hq;
+    a.hkv = m->hkv;
+    a.Il = m->Il;
+    a.L = m->L;
+    a.T = m->T;
+    a.nwg = tpl_nwg();
+    a.act_mode = m->c.act_mode;
+    a.eps = m->c.eps;
+    a.scale = 1.0f / sqrtf((float)kTlHD);
+    a.w = m->tl.w;
+    a.norms = m->norms;
+    a.kc = (__half*)m->kc;
+    a.vc = (__half*)m->vc;
+    a.sin_t = m->sin_t;
+    a.cos_t = m->cos_t;
+    a.st = m->st;
+    a.x = m->x;
+    a.g_x = m->tl.g_x;
+    a.g_qkv = m->tl.g_qkv;
+    a.g_part = m->tl.g_part;
+    a.g_att = m->tl.g_att;
+    a.g_x1 = m->tl.g_x1;
+    a.g_act = m->tl.g_act;
+    a.epoch = m->tl.epoch;
+    a.rank = m->c.tp_rank;
+    a.nranks = m->c.tp_size;
+    a.mode = !m->partial ? 0 : (m->os_open ? 2 : 1);
+    a.loopback = m->os_loopback ? 1 : 0;
+    a.xg = m->tl.xg;  // mode 2: every rank's exchange granules inside its comm buffer (tpl_prepare)
+    const int G = m->hq / m->hkv;
+    if (G == 1)
+        hipLaunchKernelGGL(tp_layers_kernel<1>, dim3(a.nwg), dim3(kTlThreads), 0, m->stream, a);
+    else if (G == 2)
+        hipLaunchKernelGGL(tp_layers_kernel<2>, dim3(a.nwg), dim3(kTlThreads), 0, m->stream, a);
+    else
+        hipLaunchKernelGGL(tp_layers_kernel<4>, dim3(a.nwg), dim3(kTlThreads), 0, m->stream, a);
+    SLI_HIP(hipGetLastError());
+    return SLI_OK;
+}
 
 template <typename WT, typename KT>
 struct StepRecorder {
@@ -830,9 +963,16 @@ struct StepRecorder {
 
     // one model and its own communicator (none, RCCL, or the debug modes)
     static int record(sli_model* m) {
-        for (int p = 0; p < 2 * m->L; ++p) {
-            SLI_TRY(record_phase(m, p));
-            SLI_TRY(allreduce_x(m));
+        if (m->exec == SLI_EXEC_PERSIST) {  // embedding, then every layer in one persistent launch (tp_layers.h)
+            if constexpr (!std::is_same<WT, __half>::value || !std::is_same<KT, __half>::value)
+                return fail(SLI_ERR_STATE, "persistent layers: fp16 weights and K/V cache only");
+            SLI_TRY(embedding_launch(0, &m->st->token, m->emb, m->c.w_dtype, m->emb_s, m->x, m->V, m->D, m->stream));
+            SLI_TRY(tpl_launch(m));
+        } else {
+            for (int p = 0; p < 2 * m->L; ++p) {
+                SLI_TRY(record_phase(m, p));
+                SLI_TRY(allreduce_x(m));
+            }
         }
         if (m->ar_mode != SLI_ALLREDUCE_RCCL) {  // the argmax keys through the one-shot exchange
             SLI_TRY(record_head(m, true));
@@ -1128,6 +1268,7 @@ static int bg_sync_tiles(sli_model* m) {
 static int capture(sli_model* m) {
     if (m->comm_dead) return fail(SLI_ERR_COMM, "the RCCL communicator was aborted by an earlier bounded wait");
     SLI_TRY(bg_sync_tiles(m));
+    if (m->exec == SLI_EXEC_PERSIST && !m->graph_exec) SLI_TRY(tpl_prepare(m));
     return capture_graph(m->stream, m->graph, m->graph_exec, [&]() { return SLI_DISPATCH(m, record, m); });
 }
 
@@ -1221,6 +1362,7 @@ static int check_device_errors(sli_model* m) {
     std::string why;
     if (bits & kOsErrTimeout) why += " one-shot all-reduce timed out (the one-shot path is now refused);";
     if (bits & kAttnErrHand) why += " fused q/k/v + attention hand-off wait timed out;";
+    if (bits & kTlErrWait) why += " a persistent-layer wait timed out (a peer or a workgroup never arrived);";
     return fail(SLI_ERR_STATE, "device error bits 0x" + std::to_string(bits) + ":" + why + " outputs are stale");
 }
 
@@ -1828,8 +1970,12 @@ int sli_model_get_history(sli_model* m, int32_t seq, int32_t n, int32_t* out) {
 
 int sli_model_set_exec(sli_model* m, int32_t mode) {
     SLI_CHECK(m, SLI_ERR_ARG, "null model");
-    SLI_CHECK(mode == SLI_EXEC_LAUNCHES, SLI_ERR_ARG,
-              "unknown execution mode (the persistent one-launch step was removed in round 5: DESIGN.md §9)");
+    SLI_CHECK(mode == SLI_EXEC_LAUNCHES || mode == SLI_EXEC_PERSIST, SLI_ERR_ARG,
+              "unknown execution mode (the persistent one-launch step, mode 1, was removed in round 5: DESIGN.md §9)");
+    if (mode == SLI_EXEC_PERSIST) {
+        std::string why;
+        SLI_CHECK(tpl_check(m, &why), SLI_ERR_STATE, "persistent layers: " + why);
+    }
     SLI_HIP(hipSetDevice(m->c.device));
     if (mode != m->exec) {  // re-capture the step graph on the next step
         SLI_TRY(wait_stream(m));
@@ -2072,8 +2218,8 @@ int sli_model_set_allreduce(sli_model* m, int32_t mode) {
     // the fp32 sum moves float4s and the key exchange 2*B floats: both must fit the slot exactly
     SLI_CHECK(mode == SLI_ALLREDUCE_RCCL || ((m->B * m->D) % 4 == 0 && m->B * m->D <= m->os_nmax && 2 * m->B <= m->os_nmax),
               SLI_ERR_SHAPE, "one-shot all-reduce: B*D must be a multiple of 4 within the comm slot");
-    SLI_CHECK(mode == SLI_ALLREDUCE_RCCL || m->exec == SLI_EXEC_LAUNCHES, SLI_ERR_STATE,
-              "tensor parallelism runs the launch graph");
+    SLI_CHECK(m->exec == SLI_EXEC_LAUNCHES || mode == SLI_ALLREDUCE_FUSED_WG, SLI_ERR_STATE,
+              "the persistent layers exchange per workgroup inside the launch: fused_wg (set_exec(launches) first)");
     if (mode != m->ar_mode) {
         SLI_TRY(wait_stream(m));
         if (m->graph_exec) (void)hipGraphExecDestroy(m->graph_exec);

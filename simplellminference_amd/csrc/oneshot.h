@@ -41,9 +41,10 @@ __device__ __forceinline__ bool os_gave_up(DevState* st, unsigned spins) {
 constexpr int kOsMaxWg = 512;
 constexpr int kOsRegions = 5;
 constexpr size_t kOsDataOff = 256 + sizeof(unsigned) * kOsRegions * 2 * kOsMaxWg * kOsMaxRanks;
-inline size_t os_buffer_bytes(int nmax) {
-    return kOsDataOff + sizeof(float) * (2 + 2 * kOsRegions) * (size_t)kOsMaxRanks * nmax;
-}
+// after the data blocks: the persistent layer stack's exchange granules (tp_layers.h), 8-byte {value, tag} per row,
+// [region 2][kOsMaxRanks][nmax]
+inline size_t os_gran_off(int nmax) { return kOsDataOff + sizeof(float) * (2 + 2 * kOsRegions) * (size_t)kOsMaxRanks * nmax; }
+inline size_t os_buffer_bytes(int nmax) { return os_gran_off(nmax) + 8 * 2 * (size_t)kOsMaxRanks * nmax; }
 
 struct OneShotArgs {
     char* peers[kOsMaxRanks];  // every rank's comm buffer, mapped in this process (own one included)

@@ -44,6 +44,9 @@ PRESETS = {
     # tiny shapes wide enough for tensor parallelism over 8 ranks (heads and kv heads divisible by 8)
     "tiny-h8": LlamaModelConfig(512, 64, 512, 512, 1024, 64, 2, 8, 8, 1e-5, 10000.0),
     "tiny-gqa-h16": LlamaModelConfig(512, 64, 1024, 512, 2048, 64, 2, 16, 8, 1e-5, 10000.0),
+    # small head_dim-128 shapes for the persistent layer stack (tp_layers.h: head_dim 128, per-CU shares that fit)
+    "small-h128": LlamaModelConfig(1000, 128, 1024, 1024, 2816, 512, 2, 8, 8, 1e-5, 10000.0),
+    "small-h128-gqa": LlamaModelConfig(1000, 128, 1024, 512, 2816, 512, 2, 8, 4, 1e-5, 10000.0),
     # configs[1..3]: Llama-2 7B (public model card shape), ctx 2048
     "llama2-7b": LlamaModelConfig(32000, 128, 4096, 4096, 11008, 2048, 32, 32, 32, 1e-5, 10000.0),
     # configs[4]: Llama-3 8B (GQA), ctx 4096
@@ -164,11 +167,14 @@ class LlamaModel:
         return max(0, min(chunk, c.vocab_size - self.tp_rank * chunk))
 
     # ------------------------------------------------------------------ execution
-    EXEC = {"launches": 0}
+    EXEC = {"launches": 0, "persist": 2}
 
     def set_exec(self, mode: str) -> "LlamaModel":
-        """"launches": one graph of fused launches (the only mode since round 5). Any other name (e.g. the removed
-        "persistent") goes to the C layer as an unknown mode, which raises SliError(SLI_ERR_ARG) with its message."""
+        """"launches": one graph of fused launches per layer; "persist": the embedding, every layer as ONE persistent
+        launch (csrc/tp_layers.h; batch-1 fp16 models at head_dim 128 whose per-CU shares fit, e.g. the TP-4 / TP-8
+        shards of Llama-2-7B; under tensor parallelism after set_allreduce("fused_wg") or without a communicator),
+        then the LM head. Any other name (e.g. the removed "persistent") goes to the C layer as an unknown mode, which
+        raises SliError(SLI_ERR_ARG) with its message."""
         call("sli_model_set_exec", self._h, self.EXEC.get(mode, -1))
         return self
 

@@ -2,8 +2,10 @@
 (SLI_DEBUG_NOCOMM: the rank's kernels at their real shapes, no RCCL all-reduces; values are not a model).
 Estimates the compute part of config C2 (Llama-2-7B at TP N); the collectives come on top.
     python tools/tp_rank_time.py [N ...]
-TP_AR=oneshot|fused: the rank's all-reduces included, in loopback (SLI_DEBUG_OS_LOOPBACK: the exchange kernels
-run against the rank's own comm buffer, every flag raised locally — everything but the xGMI hop).
+TP_AR=oneshot|fused|fused_wg: the rank's all-reduces included, in loopback (SLI_DEBUG_OS_LOOPBACK: the exchange
+kernels run against the rank's own comm buffer, every flag raised locally — everything but the xGMI hop).
+TP_EXEC=persist: the layer stack as one persistent launch (csrc/tp_layers.h; with TP_AR=fused_wg its in-launch
+granule exchange in loopback).
 """
 import os
 import sys
@@ -28,6 +30,8 @@ for world in [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]:
     if ar and world > 1:
         os.environ["SLI_DEBUG_OS_LOOPBACK"] = "1"
         m.set_allreduce(ar)
+    if os.environ.get("TP_EXEC"):
+        m.set_exec(os.environ["TP_EXEC"])
     for b in range(BATCH):
         m.set_state_seq(b, 1234 + 17 * b, CTX - 1, advance=False)
     for _ in range(10):
@@ -44,5 +48,4 @@ for world in [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]:
     qa = {0: "", 1: " qkv+attn fused", 2: " qkv+attn+wo fused"}[m.fused_qkv_attn()]
     print(f"{tag}tp{world} rank {world - 1} [{m.exec_mode()}{qa}]: {ms:.3f} ms/step compute ({what}); device error "
           f"{m.state()['error']}", flush=True)
-    m.close()
     m.close()
