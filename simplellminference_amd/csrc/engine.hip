@@ -481,9 +481,11 @@ static int tpl_check(const sli_model* m, std::string* why) {
     if (m->hd != kTlHD) return no("head_dim 128 only");
     const int G = m->hq / m->hkv;
     if (!(G == 1 || G == 2 || G == 4)) return no("1, 2 or 4 query heads per kv head");
-    if (m->D % 8 || m->Il % 8 || m->D > kTlMaxX || m->Il > kTlMaxX || m->hq * kTlHD > kTlMaxX)
-        return no("D and the local FFN width must be multiples of 8 and at most 8192");
+    if (m->D % 8 || m->Il % 8 || m->D > kTlMaxD || m->Il > kTlMaxX || m->hq * kTlHD > kTlMaxX)
+        return no("D at most 4096 and the local FFN width at most 8192, both multiples of 8");
     if ((m->T + kTlKS - 1) / kTlKS > kTlMaxSplits) return no("context at most 8192");
+    auto pow2 = [](int k) { return k >= 8 && k <= 4096 && (k & (k - 1)) == 0; };
+    if (!pow2(m->D) || !pow2(m->hq * kTlHD)) return no("D and the local q width must be powers of two (fixed column groups)");
     const int nwg = tpl_nwg();
     auto cdiv = [](long long a, long long b) { return (int)((a + b - 1) / b); };
     const int nrow = cdiv(m->D, nwg), nq = cdiv((long long)(m->hq + 2 * m->hkv) * (kTlHD / 2), nwg),

@@ -193,6 +193,9 @@ static int attn_mfma_launch(AttnArgs<__half> a, int g, int T, hipStream_t s) {
     a.ppwg = kAmWgKeys * tpw;
     a.max_splits = (T + a.ppwg - 1) / a.ppwg;
     if (a.max_splits > kAttnMaxWgSplits) return fail(SLI_ERR_SHAPE, "mha: context too long for the split merge");
+    // the partial buffer (mha_part_bytes) holds the splits of the finest geometry, the fp32 cache's; a finer split
+    // here would store past it (the round-5 fault record)
+    if (a.ppwg < attn_wg_positions(SLI_DT_F32, HD)) return fail(SLI_ERR_SHAPE, "mha: split finer than the partial buffer");
     if (a.defer_merge == 2) a.defer_merge = 0;
     const int blocks = a.n_kv_heads * a.max_splits, nbuf = tpw > 1 ? 2 : 1;
     switch (g) {

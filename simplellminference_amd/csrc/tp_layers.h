@@ -39,6 +39,7 @@ constexpr int kTlHD = 128;                      // head_dim
 constexpr int kTlKS = 128;                      // keys per attention split: K and V are 8 vectors per thread
 constexpr int kTlMaxG = 4;                      // q heads per kv head
 constexpr int kTlMaxX = 8192;                   // LDS input vector (D, hq hd, Il)
+constexpr int kTlMaxD = 4096;                   // model width (the norm weights a thread needs sit in 8 registers)
 constexpr int kTlPartMax = 12288;               // per-(row, 8-column group) partial sums of one op in LDS
 constexpr int kTlMaxRows = 256;                 // rows of x a workgroup owns (D / nwg)
 constexpr int kTlMaxSplits = 64;                // T <= 8192
@@ -74,11 +75,14 @@ struct TlArgs {
     tl_u2* const* xg;         // [nranks] device table: every rank's exchange granules [2][kOsMaxRanks][D], mapped here
     unsigned long long* stamps = nullptr;  // tools/tl_lab (TL_STAMPS builds): [nwg][L][kTlStamps] s_memrealtime
 };
-constexpr int kTlStamps = 10;
+constexpr int kTlStamps = 20;
 #ifdef TL_STAMPS
+#define TL_STAMPL(lay, k) \
+    if (a.stamps && threadIdx.x == 0) a.stamps[((size_t)blockIdx.x * a.L + (lay)) * kTlStamps + (k)] = __builtin_amdgcn_s_memrealtime()
 #define TL_STAMP(k) \
     if (a.stamps && threadIdx.x == 0) a.stamps[((size_t)blockIdx.x * a.L + l) * kTlStamps + (k)] = __builtin_amdgcn_s_memrealtime()
 #else
+#define TL_STAMPL(lay, k)
 #define TL_STAMP(k)
 #endif
 
@@ -87,11 +91,21 @@ struct TlSmem {
     float part[kTlPartMax];   // GEMV partial sums; the attention's wave partials and the merge's split partials
     float rows[kTlMaxRows];   // the op's row sums (<= 256 rows per workgroup per op at the supported shapes)
     float xres[kTlMaxRows];   // the residual rows this workgroup owns (x, then x1)
-    float qv[kTlMaxG * kTlHD];
-    float kn[kTlHD], vn[kTlHD];  // this step's K / V row (the split that holds the position)
+    float qv[(kTlMaxG + 2) * kTlHD];  // the kv head's G q rows, then (the split holding pos) this step's K and V rows
     float red[2 * kTlWaves * kTlMaxG + 8];
+    unsigned vote[2][kTlWaves];  // tl_any: one flag per wave, double-buffered by call parity
+    float vsum[2][kTlWaves];     // tl_any: one partial sum per wave beside its flag (the gathers' sums of squares)
     int dead;
 };
+
+// a pointer read from device memory, declared uniform: a buffer resource built from a VGPR pointer makes the compiler
+// wrap every load in a waterfall loop (readfirstlane, compare, branch per load)
+template <class T>
+__device__ __forceinline__ T* tl_uniform(T* p) {
+    const unsigned long long v = (unsigned long long)p;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    return (T*)(((unsigned long long)hi << 32) | lo);
+}
 
 // ---------------------------------------------------------------- granules
 __device__ __forceinline__ void tl_put(tl_u2* g, int i, float v, unsigned tag) {
@@ -99,46 +113,130 @@ __device__ __forceinline__ void tl_put(tl_u2* g, int i, float v, unsigned tag) {
     __builtin_amdgcn_raw_buffer_store_b64(tl_u2{__float_as_uint(v), tag}, rs, 8u * (unsigned)i, 0, 16 /* sc1 */);
 }
 
-// n granules g[0 .. n) carrying `tag` into dst[0 .. n) (LDS), all threads; blocks of 8 per thread per sweep
-__device__ __forceinline__ void tl_gather(TlSmem& sm, const tl_u2* g, int n, unsigned tag, float* dst, DevState* st) {
+// block-wide OR with ONE barrier (__syncthreads_or costs three): each wave's ballot, one flag per wave in LDS, read by
+// all. The flags alternate between two slots by call parity: a wave writing call k + 2's flags has passed call k + 1's
+// barrier, which every wave reaches only after reading call k's.
+template <bool SUM = false>
+__device__ __forceinline__ bool tl_any(TlSmem& sm, unsigned& vp, bool v, float* sum = nullptr) {
+    const unsigned par = vp & 1u;
+    ++vp;
+    const bool w = __ballot(v) != 0;
+    float ws = 0.0f;
+    if constexpr (SUM) ws = wave_sum(*sum);
+    if ((tl_tid() & 63) == 0) {
+        sm.vote[par][tl_tid() >> 6] = w ? 1u : 0u;
+        if constexpr (SUM) sm.vsum[par][tl_tid() >> 6] = ws;
+    }
+    __syncthreads();
+    const uint4 f0 = *reinterpret_cast<const uint4*>(&sm.vote[par][0]);
+    const uint4 f1 = *reinterpret_cast<const uint4*>(&sm.vote[par][4]);
+    if constexpr (SUM) {
+        const float4 s0 = *reinterpret_cast<const float4*>(&sm.vsum[par][0]);
+        const float4 s1 = *reinterpret_cast<const float4*>(&sm.vsum[par][4]);
+        *sum = ((((((s0.x + s0.y) + s0.z) + s0.w) + s1.x) + s1.y) + s1.z) + s1.w;
+    }
+    return (f0.x | f0.y | f0.z | f0.w | f1.x | f1.y | f1.z | f1.w) != 0;
+}
+
+// the bounded-wait give-up of every gather, checked every 1024 passes: true once this one has swept kTlSpin times, or
+// another workgroup (or rank) gave up already; then the workgroup skips every later wait and the grid drains
+__device__ __forceinline__ bool tl_give_up(TlSmem& sm, unsigned& vp, DevState* st, unsigned pass) {
+    if ((pass & 1023u) != 1023u) {
+        __builtin_amdgcn_s_sleep(1);
+        return false;
+    }
+    bool give_up = pass >= kTlSpin;
+    if (tl_tid() == 0)
+        give_up = give_up || (__hip_atomic_load(&st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & kTlErrWait) != 0;
+    if (tl_any(sm, vp, give_up)) {
+        if (tl_tid() == 0) {
+            __hip_atomic_fetch_or(&st->error, kTlErrWait, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            sm.dead = 1;
+        }
+        __syncthreads();
+        return true;
+    }
+    return false;
+}
+
+// n granules g[0 .. n) carrying `tag` into dst[0 .. n) (LDS), all threads, up to 8 per thread per sweep. Branch-free
+// sweep (instruction count is what a persistent layer pays for, tools/tl_lab): every pass loads all of the thread's
+// granules (indices past n clamped to n - 1) and stores every value; a value stored before its tag arrived is
+// overwritten by a later pass, and the loop ends on the pass where every tag matched. (A tag never moves past this
+// edge's while the gather runs: its producers' next write needs this workgroup's later output.) The last tl_any's
+// barrier publishes dst.
+template <bool SS = false>
+__device__ __forceinline__ void tl_gather(TlSmem& sm, unsigned& vp, const tl_u2* g, int n, unsigned tag, float* dst, DevState* st,
+                                          float* ss = nullptr) {
     if (sm.dead) return;
     const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<tl_u2*>(g), 0, 0x7fffffff, 0x00020000);
     constexpr int kPer = 8;
+    const int tid = tl_tid();
     for (int b0 = 0; b0 < n; b0 += kPer * kTlThreads) {
-        unsigned todo = 0;
+        unsigned off[kPer];
 #pragma unroll
-        for (int j = 0; j < kPer; ++j)
-            if (b0 + tl_tid() + j * kTlThreads < n) todo |= 1u << j;
+        for (int j = 0; j < kPer; ++j) off[j] = (unsigned)min(b0 + tid + j * kTlThreads, n - 1);
         for (unsigned pass = 0;; ++pass) {
             tl_u2 v[kPer];
 #pragma unroll
-            for (int j = 0; j < kPer; ++j)
-                if (todo & (1u << j))
-                    v[j] = __builtin_amdgcn_raw_buffer_load_b64(rs, 8u * (unsigned)(b0 + tl_tid() + j * kTlThreads), 0,
-                                                                16 /* sc1 */);
+            for (int j = 0; j < kPer; ++j) v[j] = __builtin_amdgcn_raw_buffer_load_b64(rs, 8u * off[j], 0, 16 /* sc1 */);
+            bool miss = false;
+            float sq = 0.0f;  // (SS: RMSNorm's sum of squares of this pass's values; the last pass's is the one kept)
 #pragma unroll
-            for (int j = 0; j < kPer; ++j)
-                if ((todo & (1u << j)) && v[j].y == tag) {
-                    dst[b0 + tl_tid() + j * kTlThreads] = __uint_as_float(v[j].x);
-                    todo &= ~(1u << j);
-                }
-            if (__syncthreads_or(todo != 0) == 0) break;
-            bool give_up = pass >= kTlSpin;
-            if ((pass & 1023u) == 1023u && tl_tid() == 0)  // another workgroup (or rank) gave up: stop now
-                give_up = give_up || (__hip_atomic_load(&st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) &
-                                      kTlErrWait) != 0;
-            if (__syncthreads_or(give_up)) {
-                if (tl_tid() == 0) {
-                    __hip_atomic_fetch_or(&st->error, kTlErrWait, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    sm.dead = 1;
-                }
-                __syncthreads();
-                return;
+            for (int j = 0; j < kPer; ++j) {
+                miss |= v[j].y != tag;
+                const float x = __uint_as_float(v[j].x);
+                dst[off[j]] = x;
+                if constexpr (SS) sq += b0 + tid + j * kTlThreads < n ? x * x : 0.0f;
             }
-            __builtin_amdgcn_s_sleep(1);
+            if constexpr (SS) {
+                if (!tl_any<true>(sm, vp, miss, &sq)) {
+                    *ss += sq;
+                    break;
+                }
+            } else {
+                if (!tl_any(sm, vp, miss)) break;
+            }
+            if (tl_give_up(sm, vp, st, pass)) return;
         }
     }
-    __syncthreads();
+}
+
+// two granule sets in one sweep: n1 contiguous from g1, then n2 from g2 (blocks of inner, stride apart), into dst;
+// n1 + n2 <= 2 * kTlThreads; branch-free like tl_gather (offsets computed once per call)
+__device__ __forceinline__ void tl_gather2(TlSmem& sm, unsigned& vp, const tl_u2* g1, int n1, const tl_u2* g2, int n2, int inner,
+                                           int stride, unsigned tag, float* dst, DevState* st) {
+    if (sm.dead) return;
+    const int n = n1 + n2;
+    if (n <= 0) return;
+    const auto r1 = __builtin_amdgcn_make_buffer_rsrc(const_cast<tl_u2*>(g1 ? g1 : g2), 0, 0x7fffffff, 0x00020000);
+    const auto r2 = __builtin_amdgcn_make_buffer_rsrc(const_cast<tl_u2*>(g2), 0, 0x7fffffff, 0x00020000);
+    const int tid = tl_tid();
+    int idx[2];
+    unsigned off[2];
+    bool first[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        idx[j] = min(tid + j * kTlThreads, n - 1);
+        first[j] = idx[j] < n1;
+        const int k = idx[j] - n1, o = first[j] ? 0 : k / inner;
+        off[j] = 8u * (unsigned)(first[j] ? idx[j] : o * stride + (k - o * inner));
+    }
+    for (unsigned pass = 0;; ++pass) {
+        tl_u2 v[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            v[j] = first[j] ? __builtin_amdgcn_raw_buffer_load_b64(r1, off[j], 0, 16 /* sc1 */)
+                            : __builtin_amdgcn_raw_buffer_load_b64(r2, off[j], 0, 16);
+        bool miss = false;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            miss |= v[j].y != tag;
+            dst[idx[j]] = __uint_as_float(v[j].x);
+        }
+        if (!tl_any(sm, vp, miss)) break;
+        if (tl_give_up(sm, vp, st, pass)) return;
+    }
 }
 
 // ---------------------------------------------------------------- register-chunk GEMV over LDS-staged input
@@ -150,44 +248,103 @@ struct TlChunk {
     u32x4 w[CH];
 };
 
-template <int CH, class RowF>
-__device__ __forceinline__ void tl_issue(TlChunk<CH>& c, const __half* W, int K, int nr, const RowF& row, int chunk) {
-    const int G = K >> 3, nv = nr * G;
-    if (nv <= 0) return;
-    const int tid = tl_tid();
-#pragma unroll
-    for (int j = 0; j < CH; ++j) {
-        int v = (chunk * CH + j) * kTlThreads + tid;
-        v = v < nv ? v : nv - 1;  // clamped: a duplicate of a vector in flight, never a branch around a load
-        const int r = v / G, g = v - r * G;
-        c.w[j] = load16<true>(W + (size_t)row(r) * K + 8 * g);
+// (row, group) of vector v0 = (chunk CH) 512 + tid, then of v0 + 512 j, j < CH, by increments (no division per vector:
+// the kernel's loop body has to fit the instruction cache)
+struct TlVec {
+    int r, g;
+};
+__device__ __forceinline__ TlVec tl_vec0(int G, int chunk, int CH) {
+    const int v = chunk * CH * kTlThreads + tl_tid();
+    const int r = v / G;
+    return {r, v - r * G};
+}
+__device__ __forceinline__ void tl_vec_next(TlVec& p, int G, int q512, int r512) {
+    p.g += r512;
+    p.r += q512;
+    if (p.g >= G) {
+        p.g -= G;
+        p.r += 1;
     }
 }
 
-template <int CH>
-__device__ __forceinline__ void tl_consume(const TlChunk<CH>& c, int K, int nr, const float* xs, float* part, int chunk) {
-    const int G = K >> 3, nv = nr * G;
+// FIXED: K / 8 divides the 512 threads (K a power of two <= 4096: q/k/v, wo and gate/up at the supported shapes), so a
+// thread's column group is fixed and the row advances by a constant; otherwise (down: K = the local FFN width) the
+// (row, group) pair is stepped incrementally
+template <int CH, bool FIXED, class RowF>
+__device__ __forceinline__ void tl_issue(TlChunk<CH>& c, const __half* W, int K, int nr, const RowF& row, int chunk) {
+    const int G = K >> 3;
+    if (nr <= 0) return;
+    // 32-bit byte offsets into the matrix (a shard matrix is < 4 GiB): one buffer resource, no 64-bit address math
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<__half*>(W), 0, 0x7fffffff, 0x00020000);
     const int tid = tl_tid();
+    if constexpr (FIXED) {
+        const int per = kTlThreads / G, g = tid % G, r0 = chunk * CH * per + tid / G;
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const int r = min(r0 + j * per, nr - 1);  // clamped: a duplicate of a vector in flight, never a branch
+            c.w[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, 2u * ((unsigned)row(r) * (unsigned)K + 8u * (unsigned)g), 0,
+                                                           2 /* nt: streamed once */);
+        }
+    } else {
+    const int q512 = kTlThreads / G, r512 = kTlThreads - q512 * G;
+    TlVec p = tl_vec0(G, chunk, CH);
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
-        const int v = (chunk * CH + j) * kTlThreads + tid;
-        __builtin_amdgcn_sched_barrier(0);  // one vector's input loads at a time (live registers, not latency)
-        if (v < nv) {
-            const int g = v - (v / G) * G;
-            const float4 x0 = *reinterpret_cast<const float4*>(xs + 8 * g);
-            const float4 x1 = *reinterpret_cast<const float4*>(xs + 8 * g + 4);
-            const __half2* h = reinterpret_cast<const __half2*>(&c.w[j]);
-            const float2 a = __half22float2(h[0]), b = __half22float2(h[1]), e = __half22float2(h[2]),
-                         f = __half22float2(h[3]);
-            float s = a.x * x0.x;
-            s = fmaf(a.y, x0.y, s);
-            s = fmaf(b.x, x0.z, s);
-            s = fmaf(b.y, x0.w, s);
-            s = fmaf(e.x, x1.x, s);
-            s = fmaf(e.y, x1.y, s);
-            s = fmaf(f.x, x1.z, s);
-            s = fmaf(f.y, x1.w, s);
-            part[v] = s;
+        const bool in = p.r < nr;
+        const unsigned off = 2u * ((unsigned)row(in ? p.r : nr - 1) * (unsigned)K + 8u * (unsigned)(in ? p.g : G - 1));
+        c.w[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 2);
+        tl_vec_next(p, G, q512, r512);
+    }
+    }
+}
+
+__device__ __forceinline__ float tl_dot8(const u32x4& w, const float* x) {  // x: 8 floats (LDS or registers)
+    const float4 x0 = *reinterpret_cast<const float4*>(x);
+    const float4 x1 = *reinterpret_cast<const float4*>(x + 4);
+    const __half2* h = reinterpret_cast<const __half2*>(&w);
+    const float2 a = __half22float2(h[0]), b = __half22float2(h[1]), e = __half22float2(h[2]), f = __half22float2(h[3]);
+    float s = a.x * x0.x;
+    s = fmaf(a.y, x0.y, s);
+    s = fmaf(b.x, x0.z, s);
+    s = fmaf(b.y, x0.w, s);
+    s = fmaf(e.x, x1.x, s);
+    s = fmaf(e.y, x1.y, s);
+    s = fmaf(f.x, x1.z, s);
+    s = fmaf(f.y, x1.w, s);
+    return s;
+}
+
+template <int CH, bool FIXED>
+__device__ __forceinline__ void tl_consume(const TlChunk<CH>& c, int K, int nr, const float* xs, float* part, int chunk,
+                                           const float* nw) {
+    const int G = K >> 3;
+    const int tid = tl_tid();
+    if constexpr (FIXED) {
+        const int per = kTlThreads / G, g = tid % G, r0 = chunk * CH * per + tid / G;
+        // the thread's 8 inputs, once (times their norm weights where the op is RMS-normalised: the row sums are scaled
+        // by 1/rms afterwards)
+        float xr[8];
+        {
+            const float4 x0 = *reinterpret_cast<const float4*>(xs + 8 * g), x1 = *reinterpret_cast<const float4*>(xs + 8 * g + 4);
+            xr[0] = x0.x, xr[1] = x0.y, xr[2] = x0.z, xr[3] = x0.w, xr[4] = x1.x, xr[5] = x1.y, xr[6] = x1.z, xr[7] = x1.w;
+            if (nw) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) xr[e] *= nw[e];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            // clamped like the loads: a vector past the last is a duplicate of it, its dot the same value (no branch)
+            const int r = min(r0 + j * per, nr - 1);
+            part[r * G + g] = tl_dot8(c.w[j], xr);
+        }
+    } else {
+        const int q512 = kTlThreads / G, r512 = kTlThreads - q512 * G;
+        TlVec p = tl_vec0(G, chunk, CH);
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            if (p.r < nr) part[p.r * G + p.g] = tl_dot8(c.w[j], xs + 8 * p.g);
+            tl_vec_next(p, G, q512, r512);
         }
     }
 }
@@ -195,46 +352,56 @@ __device__ __forceinline__ void tl_consume(const TlChunk<CH>& c, int K, int nr, 
 // the whole op: chunk 0 already issued into c (before the input edge); a larger share's later chunks follow one by
 // one (one register set: the TP-4 / TP-8 shards are one chunk per op). Row sums into sm.rows[0 .. nr), each summed
 // over its groups in group order by one wave (deterministic).
-template <int CH, class RowF>
-__device__ __forceinline__ void tl_gemv(TlSmem& sm, TlChunk<CH>& c, const __half* W, int K, int nr, const RowF& row) {
+template <int CH, bool FIXED, class RowF>
+__device__ __forceinline__ void tl_gemv(TlSmem& sm, TlChunk<CH>& c, const __half* W, int K, int nr, const RowF& row,
+                                        const float* nw = nullptr, float scale = 1.0f) {
     const int G = K >> 3, nch = (nr * G + CH * kTlThreads - 1) / (CH * kTlThreads);
+#pragma nounroll
     for (int ch = 0; ch < nch; ++ch) {
-        if (ch > 0) tl_issue(c, W, K, nr, row, ch);
-        tl_consume(c, K, nr, sm.xs, sm.part, ch);
+        if (ch > 0) tl_issue<CH, FIXED>(c, W, K, nr, row, ch);
+        tl_consume<CH, FIXED>(c, K, nr, sm.xs, sm.part, ch, nw);
     }
     __syncthreads();
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = tl_tid() & 63, wave = tl_tid() >> 6;
     for (int i = wave; i < nr; i += kTlWaves) {
         float s = 0.0f;
-        for (int g = lane; g < G; g += 64) s += sm.part[i * G + g];
+        if (G <= 8 * 64) {  // (every op at the supported shapes) independent loads, no loop-carried branch
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int g = lane + 64 * k;
+                const float v = sm.part[i * G + min(g, G - 1)];
+                s += g < G ? v : 0.0f;
+            }
+        } else {
+            for (int g = lane; g < G; g += 64) s += sm.part[i * G + g];
+        }
         s = wave_sum(s);
-        if (lane == 0) sm.rows[i] = s;
+        if (lane == 0) sm.rows[i] = s * scale;
     }
     __syncthreads();
 }
 
-// x (n = D floats in sm.xs) -> RMSNorm in place (rms_kernel.cpp:5-23: y = (x * 1/sqrt(mean(x^2) + eps)) * w)
-__device__ __forceinline__ void tl_rmsnorm(TlSmem& sm, int D, const float* w, float eps) {
-    float ss = 0.0f;
-    for (int i = tl_tid(); i < D; i += kTlThreads) ss += sm.xs[i] * sm.xs[i];
-    ss = wave_sum(ss);
-    if ((tl_tid() & 63) == 0) sm.red[tl_tid() >> 6] = ss;
-    __syncthreads();
-    if (tl_tid() == 0) {
-        float t = 0.0f;
-        for (int k = 0; k < kTlWaves; ++k) t += sm.red[k];
-        sm.red[kTlWaves] = 1.0f / sqrtf(t / (float)D + eps);
-    }
-    __syncthreads();
-    const float inv = sm.red[kTlWaves];
-    for (int i = tl_tid(); i < D; i += kTlThreads) sm.xs[i] = (sm.xs[i] * inv) * w[i];
-    __syncthreads();
+// the norm weights a thread multiplies (w[t + 512 k], k < D / 512, D <= 4096): loaded before the input edge, so the
+// RMSNorm after it pays no global round trip
+struct TlNormW {
+    float w[kTlMaxD / kTlThreads];  // the norm weights of the thread's 8 columns (its fixed group of the D-wide GEMV)
+};
+__device__ __forceinline__ void tl_issue_norm(TlNormW& n, const float* w, int D) {
+    const int g = tl_tid() % (D >> 3);  // D / 8 divides 512 (tpl_check): the thread's column group of every D-wide GEMV
+    const float4 a = *reinterpret_cast<const float4*>(w + 8 * g), b = *reinterpret_cast<const float4*>(w + 8 * g + 4);
+    n.w[0] = a.x, n.w[1] = a.y, n.w[2] = a.z, n.w[3] = a.w, n.w[4] = b.x, n.w[5] = b.y, n.w[6] = b.z, n.w[7] = b.w;
 }
+
+// RMSNorm (rms_kernel.cpp:5-23: y = (x * 1/sqrt(mean(x^2) + eps)) * w) is folded into the D-wide GEMVs: the gather
+// sums the squares, the consume multiplies each x by its column's norm weight (kept in registers) and the row sums
+// are scaled by 1/rms, so the normalised vector is never written (one LDS pass and two barriers per norm fewer; the
+// products round as inv * sum(W x w) instead of sum(W ((x inv) w)): within the parity bar, tests/test_gpu_tp_layers.py)
+__device__ __forceinline__ float tl_rms_inv(float ss, int D, float eps) { return 1.0f / sqrtf(ss / (float)D + eps); }
 
 // ---------------------------------------------------------------- residual exchange of this workgroup's rows
 // val[i] (LDS sm.rows) = this rank's projection rows r0 + i; out: sm.xres[i] = the new residual rows. Region 0: wo,
 // 1: down.
-__device__ __forceinline__ void tl_exchange(TlSmem& sm, const TlArgs& a, int r0, int nrow, int region, unsigned tag) {
+__device__ __forceinline__ void tl_exchange(TlSmem& sm, unsigned& vp, const TlArgs& a, int r0, int nrow, int region, unsigned tag) {
     const int t = tl_tid();
     if (a.mode == 0) {  // one rank: x += projection (EpiStore: resid + acc)
         if (t < nrow) sm.xres[t] = sm.xres[t] + sm.rows[t];
@@ -252,15 +419,18 @@ __device__ __forceinline__ void tl_exchange(TlSmem& sm, const TlArgs& a, int r0,
     if (t < nrow) {
         for (int p = 0; p < a.nranks; ++p) {
             // slot [rank] of every rank's buffer; loopback (one process, every "peer" this rank): every slot of its own
-            tl_u2* dst = a.loopback ? a.xg[a.rank] + ((size_t)region * 8 + p) * D
-                                    : a.xg[p] + ((size_t)region * 8 + a.rank) * D;
+            tl_u2* dst = a.loopback ? tl_uniform(a.xg[a.rank]) + ((size_t)region * 8 + p) * D
+                                    : tl_uniform(a.xg[p]) + ((size_t)region * 8 + a.rank) * D;
             tl_put(dst, r0 + t, v, tag);
         }
+        // the pushes acknowledged before this workgroup's first poll of its own slots, so that poll is not wasted on
+        // its own stores still in flight (uncached memory: each poll is a full memory round trip)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     // this workgroup's rows of every rank's slot in its own buffer, summed in rank order
-    float* got = sm.part;  // [nranks][nrow]
-    for (int p = 0; p < a.nranks; ++p)
-        tl_gather(sm, a.xg[a.rank] + ((size_t)region * 8 + p) * D + r0, nrow, tag, got + p * nrow, a.st);
+    float* got = sm.part;  // [nranks][nrow], one sweep over every slot
+    tl_gather2(sm, vp, nullptr, 0, tl_uniform(a.xg[a.rank]) + (size_t)region * 8 * D + r0, a.nranks * nrow, nrow, (int)D, tag,
+               got, a.st);
     if (t < nrow) {
         float s = got[t];
         for (int p = 1; p < a.nranks; ++p) s += got[p * nrow + t];
@@ -296,12 +466,13 @@ __device__ __forceinline__ u32x4 tl_pack8(const float* p) {
 }
 
 template <int G>
-__device__ __forceinline__ void tl_attend(TlSmem& sm, const TlArgs& a, TlKV& r, int kvh, int s, int S, int pos, unsigned tag) {
+__device__ __forceinline__ void tl_attend(TlSmem& sm, const TlArgs& a, TlKV& r, int kvh, int s, int S, int pos, unsigned tag,
+                                          int lay) {
     const int t = tl_tid(), c = t & 15, lane = t & 63, wave = t >> 6;
     const int k0 = s * kTlKS;
     if (pos >= k0 && pos < k0 + kTlKS) {  // this step's row replaces the cache's (fp16, as the cache stores it)
         const int jj = pos - k0 - (t >> 4);
-        const u32x4 kn = tl_pack8(sm.kn + 8 * c), vn = tl_pack8(sm.vn + 8 * c);
+        const u32x4 kn = tl_pack8(sm.qv + G * kTlHD + 8 * c), vn = tl_pack8(sm.qv + (G + 1) * kTlHD + 8 * c);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {  // selects, not a conditional store (that became an indexed one: scratch)
             const bool hit = jj == 32 * j;
@@ -331,6 +502,7 @@ __device__ __forceinline__ void tl_attend(TlSmem& sm, const TlArgs& a, TlKV& r, 
             sc[j][g] = key <= pos ? d * a.scale : -INFINITY;
         }
     }
+    TL_STAMPL(lay, 16);
     // split max and sum per q head: a lane's 4 keys, the wave's 4 key groups (lanes 16 apart), then the 8 waves
     float mx[G];
 #pragma unroll
@@ -346,6 +518,7 @@ __device__ __forceinline__ void tl_attend(TlSmem& sm, const TlArgs& a, TlKV& r, 
         for (int w = 1; w < kTlWaves; ++w) m = fmaxf(m, sm.red[w * G + g]);
         mx[g] = m;  // finite: key k0 <= pos is live
     }
+    TL_STAMPL(lay, 17);
     float p[4][G], ls[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -382,6 +555,7 @@ __device__ __forceinline__ void tl_attend(TlSmem& sm, const TlArgs& a, TlKV& r, 
         }
     }
     __syncthreads();  // (red[] of the max is read above; the l sums go to red[] below, after this barrier)
+    TL_STAMPL(lay, 18);
     if (lane == 0) {
 #pragma unroll
         for (int g = 0; g < G; ++g) sm.red[kTlWaves * kTlMaxG + wave * G + g] = ls[g];
@@ -410,21 +584,37 @@ __device__ __forceinline__ void tl_attend(TlSmem& sm, const TlArgs& a, TlKV& r, 
 // the kv head's merge: ns live splits per q head -> attention output rows (attention.h attn_merge: M = max m_s,
 // w_s = e^{m_s - M}, out = sum w_s o_s / sum w_s l_s, in split order)
 template <int G>
-__device__ __forceinline__ void tl_merge(TlSmem& sm, const TlArgs& a, int kvh, int S, int ns, unsigned tag_in, unsigned tag_out) {
+__device__ __forceinline__ void tl_merge(TlSmem& sm, unsigned& vp, const TlArgs& a, int kvh, int S, int ns, unsigned tag_in, unsigned tag_out,
+                                         int lay) {
     for (int g = 0; g < G; ++g) {
         const int h = kvh * G + g;
-        tl_gather(sm, a.g_part + (size_t)h * S * kTlPart, ns * kTlPart, tag_in, sm.part, a.st);
-        const int d = tl_tid();
-        if (d < kTlHD) {
-            float M = -INFINITY;
-            for (int s = 0; s < ns; ++s) M = fmaxf(M, sm.part[s * kTlPart + kTlHD]);
-            float num = 0.0f, den = 0.0f;
-            for (int s = 0; s < ns; ++s) {
-                const float w = expf(sm.part[s * kTlPart + kTlHD] - M);
-                num = fmaf(w, sm.part[s * kTlPart + d], num);
-                den = fmaf(w, sm.part[s * kTlPart + kTlHD + 1], den);
+        tl_gather(sm, vp, a.g_part + (size_t)h * S * kTlPart, ns * kTlPart, tag_in, sm.part, a.st);
+#ifdef TL_STAMPS
+        if (a.stamps && threadIdx.x == 0) a.stamps[((size_t)blockIdx.x * a.L + lay) * kTlStamps + 12] = __builtin_amdgcn_s_memrealtime();
+#endif
+        // 512 threads: dim d = t & 127, quarter q = t >> 7 takes splits q, q + 4, ...; M over every split (independent
+        // broadcast reads), the quarters' sums combined in quarter order (deterministic)
+        const int t = tl_tid(), d = t & (kTlHD - 1), q = t >> 7;
+        float M = -INFINITY;
+        for (int s2 = 0; s2 < ns; ++s2) M = fmaxf(M, sm.part[s2 * kTlPart + kTlHD]);
+        float num = 0.0f, den = 0.0f;
+        for (int s2 = q; s2 < ns; s2 += kTlThreads / kTlHD) {
+            const float w = expf(sm.part[s2 * kTlPart + kTlHD] - M);
+            num = fmaf(w, sm.part[s2 * kTlPart + d], num);
+            den = fmaf(w, sm.part[s2 * kTlPart + kTlHD + 1], den);
+        }
+        float* qs = sm.part + kTlMaxSplits * kTlPart;  // [4][hd] numerators, then [4][hd] denominators
+        qs[q * kTlHD + d] = num;
+        qs[(kTlThreads / kTlHD + q) * kTlHD + d] = den;
+        __syncthreads();
+        if (t < kTlHD) {
+            float n2 = qs[d], d2 = qs[4 * kTlHD + d];
+#pragma unroll
+            for (int k = 1; k < kTlThreads / kTlHD; ++k) {
+                n2 += qs[k * kTlHD + d];
+                d2 += qs[(4 + k) * kTlHD + d];
             }
-            tl_put(a.g_att, h * kTlHD + d, num / den, tag_out);
+            tl_put(a.g_att, h * kTlHD + d, n2 / d2, tag_out);
         }
         __syncthreads();
     }
@@ -436,6 +626,7 @@ __global__ void __launch_bounds__(kTlThreads) tp_layers_kernel(TlArgs a) {
     __shared__ TlSmem sm;
     const int t = threadIdx.x, w = blockIdx.x, nwg = a.nwg;
     if (t == 0) sm.dead = 0;
+    unsigned vp = 0;  // tl_any's call parity (every thread makes the same calls)
     const int pos = a.st->pos;
     const unsigned E = *a.epoch + 1u;
     __syncthreads();
@@ -456,29 +647,46 @@ __global__ void __launch_bounds__(kTlThreads) tp_layers_kernel(TlArgs a) {
 
     for (int l = 0; l < L; ++l) {
         const unsigned tb = (E * (unsigned)L + (unsigned)l) * 8u;
-        const __half* const* W = a.w + 4 * l;
+        const __half* W[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) W[k] = tl_uniform(a.w[4 * l + k]);
         // ---- E1 -> RMSNorm -> q/k/v (+ RoPE, K/V cache rows)
         TlChunk<kTlCHQ> c;
-        tl_issue(c, W[0], D, 2 * nq, row_qkv, 0);
+        tl_issue<kTlCHQ, true>(c, W[0], D, 2 * nq, row_qkv, 0);
+        TlNormW nw;
+        tl_issue_norm(nw, a.norms + (size_t)(2 * l) * D, D);
+        float rsin = 0.0f, rcos = 1.0f;  // this thread's q/k/v unit's RoPE table entries (rope_kernel.cpp:30-38)
+        if (t < nq) {
+            const int u = q0 + t, d = u % (kTlHD / 2);
+            rsin = a.sin_t[pos * (kTlHD / 2) + d];
+            rcos = a.cos_t[pos * (kTlHD / 2) + d];
+        }
         TlKV kv;
         const bool attn_item = w < n_items && (w % S) < ns;  // (first item only in registers early)
         if (attn_item) tl_issue_kv(kv, a, l, w / S, w % S, pos);
-        if (l == 0) {
-            for (int i = t; i < D; i += kTlThreads) sm.xs[i] = a.x[i];
-            __syncthreads();
+        float ss = 0.0f;  // sum of squares of x (RMSNorm)
+        if (l == 0) {  // the embedding's x, written before this launch
+            float sq = 0.0f;
+            for (int i = t; i < D; i += kTlThreads) {
+                const float v = a.x[i];
+                sm.xs[i] = v;
+                sq += v * v;
+            }
+            tl_any<true>(sm, vp, false, &sq);  // (the block sum; its barrier publishes xs)
+            ss = sq;
         } else {
-            tl_gather(sm, a.g_x, D, tb + 1, sm.xs, a.st);
+            tl_gather<true>(sm, vp, a.g_x, D, tb + 1, sm.xs, a.st, &ss);
         }
         TL_STAMP(0);
         if (t < nrow) sm.xres[t] = sm.xs[r0 + t];
-        __syncthreads();
-        tl_rmsnorm(sm, D, a.norms + (size_t)(2 * l) * D, a.eps);
-        tl_gemv(sm, c, W[0], D, 2 * nq, row_qkv);
+        TL_STAMP(14);
+        tl_gemv<kTlCHQ, true>(sm, c, W[0], D, 2 * nq, row_qkv, nw.w, tl_rms_inv(ss, D, a.eps));
+        TL_STAMP(15);
         if (t < nq) {  // EpiQKV (rope_kernel.cpp:30-38)
             const int u = q0 + t, uh = u / (kTlHD / 2), d = u - uh * (kTlHD / 2);
             float r0v = sm.rows[2 * t], r1v = sm.rows[2 * t + 1];
             if (uh < hq + hkv) {
-                const float fci = a.sin_t[pos * (kTlHD / 2) + d], fcr = a.cos_t[pos * (kTlHD / 2) + d];
+                const float fci = rsin, fcr = rcos;
                 const float x0 = r0v * fcr - r1v * fci, x1 = r1v * fcr + r0v * fci;
                 r0v = x0;
                 r1v = x1;
@@ -499,32 +707,34 @@ __global__ void __launch_bounds__(kTlThreads) tp_layers_kernel(TlArgs a) {
             const int kvh = it / S, s = it - kvh * S;
             if (s >= ns) continue;
             if (it != w) tl_issue_kv(kv, a, l, kvh, s, pos);
-            tl_gather(sm, a.g_qkv + (size_t)kvh * G * kTlHD, G * kTlHD, tb + 2, sm.qv, a.st);
-            if (pos >= s * kTlKS && pos < s * kTlKS + kTlKS) {
-                tl_gather(sm, a.g_qkv + (size_t)(hq + kvh) * kTlHD, kTlHD, tb + 2, sm.kn, a.st);
-                tl_gather(sm, a.g_qkv + (size_t)(hq + hkv + kvh) * kTlHD, kTlHD, tb + 2, sm.vn, a.st);
-            }
-            tl_attend<G>(sm, a, kv, kvh, s, S, pos, tb + 3);
+            const bool own_row = pos >= s * kTlKS && pos < s * kTlKS + kTlKS;  // this split holds this step's K / V
+            // the G q rows, then (the split holding pos) k and v, hkv * hd apart: one sweep
+            tl_gather2(sm, vp, a.g_qkv + (size_t)kvh * G * kTlHD, G * kTlHD, a.g_qkv + (size_t)(hq + kvh) * kTlHD,
+                       own_row ? 2 * kTlHD : 0, kTlHD, hkv * kTlHD, tb + 2, sm.qv, a.st);
+            TL_STAMP(10);
+            tl_attend<G>(sm, a, kv, kvh, s, S, pos, tb + 3, l);
+            TL_STAMP(11);
         }
         for (int it = w; it < n_items; it += nwg)
-            if (it % S == 0) tl_merge<G>(sm, a, it / S, S, ns, tb + 3, tb + 4);
+            if (it % S == 0) tl_merge<G>(sm, vp, a, it / S, S, ns, tb + 3, tb + 4, l);
         TL_STAMP(2);
         // ---- wo (+ residual, exchange)
         TlChunk<kTlCHO> co;
-        tl_issue(co, W[1], hq * kTlHD, nrow, row_x, 0);
-        tl_gather(sm, a.g_att, hq * kTlHD, tb + 4, sm.xs, a.st);
+        tl_issue<kTlCHO, true>(co, W[1], hq * kTlHD, nrow, row_x, 0);
+        tl_gather(sm, vp, a.g_att, hq * kTlHD, tb + 4, sm.xs, a.st);
         TL_STAMP(3);
-        tl_gemv(sm, co, W[1], hq * kTlHD, nrow, row_x);
+        tl_gemv<kTlCHO, true>(sm, co, W[1], hq * kTlHD, nrow, row_x);
         TL_STAMP(4);
-        tl_exchange(sm, a, r0, nrow, 0, tb + 7);
+        tl_exchange(sm, vp, a, r0, nrow, 0, tb + 7);
         if (t < nrow) tl_put(a.g_x1, r0 + t, sm.xres[t], tb + 5);
         // ---- E4 -> RMSNorm -> gate/up -> SwiGLU (swiglu_kernel.cpp:12-13: sigmoid(gate) * up; act_mode 1: SiLU)
         TlChunk<kTlCHG> cg;
-        tl_issue(cg, W[2], D, 2 * ng, row_gu, 0);
-        tl_gather(sm, a.g_x1, D, tb + 5, sm.xs, a.st);
+        tl_issue<kTlCHG, true>(cg, W[2], D, 2 * ng, row_gu, 0);
+        tl_issue_norm(nw, a.norms + (size_t)(2 * l + 1) * D, D);
+        float ss1 = 0.0f;
+        tl_gather<true>(sm, vp, a.g_x1, D, tb + 5, sm.xs, a.st, &ss1);
         TL_STAMP(5);
-        tl_rmsnorm(sm, D, a.norms + (size_t)(2 * l + 1) * D, a.eps);
-        tl_gemv(sm, cg, W[2], D, 2 * ng, row_gu);
+        tl_gemv<kTlCHG, true>(sm, cg, W[2], D, 2 * ng, row_gu, nw.w, tl_rms_inv(ss1, D, a.eps));
         TL_STAMP(6);
         if (t < ng) {
             const float g = sm.rows[2 * t], up = sm.rows[2 * t + 1];
@@ -534,12 +744,12 @@ __global__ void __launch_bounds__(kTlThreads) tp_layers_kernel(TlArgs a) {
         }
         // ---- E5 -> down (+ residual x1, exchange) -> the next layer's x
         TlChunk<kTlCHD> cd;
-        tl_issue(cd, W[3], Il, nrow, row_x, 0);
-        tl_gather(sm, a.g_act, Il, tb + 6, sm.xs, a.st);
+        tl_issue<kTlCHD, false>(cd, W[3], Il, nrow, row_x, 0);
+        tl_gather(sm, vp, a.g_act, Il, tb + 6, sm.xs, a.st);
         TL_STAMP(7);
-        tl_gemv(sm, cd, W[3], Il, nrow, row_x);
+        tl_gemv<kTlCHD, false>(sm, cd, W[3], Il, nrow, row_x);
         TL_STAMP(8);
-        tl_exchange(sm, a, r0, nrow, 1, tb + 0);
+        tl_exchange(sm, vp, a, r0, nrow, 1, tb + 0);
         TL_STAMP(9);
         if (t < nrow) {
             if (l + 1 < L)

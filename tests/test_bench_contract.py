@@ -1,7 +1,9 @@
-"""The bench line contract (the task's bench.py section) on the committed round-5 bench lines (profiles/r5g_bench_*.json,
+"""The bench line contract (the task's bench.py section) on the committed round-6 bench lines (profiles/r6*_bench_c*.json,
 written by `python bench.py` on an MI355X): every required key, the roofline and cpu_baseline objects, the units and
 the arithmetic that ties them together (value x ms_per_step = global batch; frac = achieved / peak; achieved = the
-dominant family's algorithmic bytes / its launch time). CPU only: it reads JSON, runs nothing."""
+dominant family's algorithmic bytes / its launch time), and the step_ms block (SURVEY §5's p50 / p99: one HIP event
+between consecutive graph replays of the timed window; its mean against the host clock, its p50 against the mean, the
+timed window against the same process's 64-token greedy run). CPU only: it reads JSON, runs nothing."""
 import glob
 import json
 import os
@@ -9,7 +11,7 @@ import os
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LINES = sorted(glob.glob(os.path.join(ROOT, "profiles", "r5g_bench_c*.json")))
+LINES = sorted(glob.glob(os.path.join(ROOT, "profiles", "r6*_bench_c*.json")))
 BASELINE = json.load(open(os.path.join(ROOT, "BASELINE.json")))
 
 
@@ -19,7 +21,8 @@ def _load(p):
 
 
 def test_lines_present():
-    assert len(LINES) == 3, LINES
+    names = {os.path.basename(p).split("_bench_")[1] for p in LINES}
+    assert {"c1.json", "c3.json", "c4.json"} <= names, LINES
 
 
 @pytest.mark.parametrize("path", LINES, ids=[os.path.basename(p) for p in LINES])
@@ -48,7 +51,24 @@ def test_bench_line_contract(path):
     assert fams[dom]["avg_launch_us"] == pytest.approx(r["avg_launch_us"], rel=1e-3)
 
 
-@pytest.mark.parametrize("path", [p for p in LINES if not p.endswith("c3.json")],
+@pytest.mark.parametrize("path", LINES, ids=[os.path.basename(p) for p in LINES])
+def test_step_ms_block(path):
+    d = _load(path)
+    s = d["step_ms"]
+    for k in ("n", "p50", "p99", "min", "max", "mean", "first5_mean", "last5_mean", "host_clock_mean"):
+        assert k in s, k
+    assert s["n"] == d["steps"]
+    assert s["min"] <= s["p50"] <= s["p99"] <= s["max"]
+    assert s["min"] <= s["first5_mean"] <= s["max"] and s["min"] <= s["last5_mean"] <= s["max"]
+    assert s["host_clock_mean"] == pytest.approx(d["ms_per_step"], rel=1e-3)
+    # the events see the same window as the host clock; p50 within 1 % of the mean
+    assert s["mean"] == pytest.approx(s["host_clock_mean"], rel=1e-2)
+    assert s["p50"] == pytest.approx(s["mean"], rel=1e-2)
+    if "greedy_64" in d and "timed_mean_over_greedy" in d["greedy_64"]:
+        assert abs(d["greedy_64"]["timed_mean_over_greedy"] - 1.0) <= 0.01
+
+
+@pytest.mark.parametrize("path", [p for p in LINES if p.endswith("_c1.json") or p.endswith("_c4.json")],
                          ids=lambda p: os.path.basename(p))
 def test_cpu_baseline(path):
     d = _load(path)

@@ -137,15 +137,28 @@ int main(int argc, char** argv) {
     std::vector<unsigned long long> h(8ull * nwg * L * kTlStamps / 8);
     CK(hipMemcpy(h.data(), a.stamps, 8ull * nwg * L * kTlStamps, hipMemcpyDeviceToHost));
     const char* names[kTlStamps] = {"E1 x", "qkv", "attn", "E3 att", "wo", "xch+E4", "gu", "E5 act", "down", "xch"};
-    for (int wg : {0, 1, 16, 100, 200, nwg - 1}) {
+    auto med = [&](int wg, int k0, int k1) {  // median over layers 1.. of stamp k1 - stamp k0
+        std::vector<double> v;
+        for (int l = 1; l < L; ++l) {
+            const unsigned long long* q = &h[((size_t)wg * L + l) * kTlStamps];
+            if (q[k0] && q[k1]) v.push_back((double)(q[k1] - q[k0]) / 100.0);
+        }
+        std::sort(v.begin(), v.end());
+        return v.empty() ? -1.0 : v[v.size() / 2];
+    };
+    for (int wg : {0, 1, 15, 16, 100, 200, nwg - 1}) {
         if (wg >= nwg) continue;
+        printf("  wg %3d: [norm %.2f gemv %.2f epi %.2f] [E2 %.2f attend %.2f (scores %.2f max %.2f pv %.2f publish %.2f) "
+               "merge-gather %.2f merge %.2f]\n", wg,
+               med(wg, 0, 14), med(wg, 14, 15), med(wg, 15, 1), med(wg, 1, 10), med(wg, 10, 11), med(wg, 10, 16),
+               med(wg, 16, 17), med(wg, 17, 18), med(wg, 18, 11), med(wg, 11, 12), med(wg, 12, 2));
         printf("  wg %3d:", wg);
-        for (int k = 0; k < kTlStamps; ++k) {
+        for (int k = 0; k < 10; ++k) {
             std::vector<double> v;
             for (int l = 1; l < L; ++l) {
                 const unsigned long long* q = &h[((size_t)wg * L + l) * kTlStamps];
                 const unsigned long long* qp = &h[((size_t)wg * L + l - 1) * kTlStamps];
-                const unsigned long long b = k == 0 ? qp[kTlStamps - 1] : q[k - 1];
+                const unsigned long long b = k == 0 ? qp[9] : q[k - 1];
                 v.push_back((double)(q[k] - b) / 100.0);
             }
             std::sort(v.begin(), v.end());
