@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--preset", default="llama2-7b")
     ap.add_argument("--ctx", type=int, default=CTX)
     ap.add_argument("--batch", type=int, default=1, help="sequences decoding in lockstep (MFMA projections if > 1)")
+    ap.add_argument("--tp-exec", default="auto", choices=["auto", "launches", "persist"],
+                    help="N>1: the layer stack as one persistent launch per rank where it fits and validates (auto), "
+                         "or the launch graph")
     ap.add_argument("--tp-allreduce", default="auto", choices=["auto", "rccl", "oneshot", "fused", "fused_wg"],
                     help="TP all-reduce: auto = the one-shot exchange fused into the wo / down launches per "
                          "workgroup when every rank has its own GPU (else batch 1: one summing workgroup per launch, "
@@ -199,6 +202,38 @@ def _own_gpus(dist, torch, local: int, world: int) -> bool:
     return "?" not in key and len(set(keys)) == world
 
 
+def _try_persist(model, dist, torch, ref, forced: bool, B: int) -> str:
+    """The layer stack as one persistent launch per rank (csrc/tp_layers.h, exec "persist"), its residual exchange the
+    per-workgroup granule exchange over the mapped peer buffers: taken only if it fits EVERY rank's shard (a rank that
+    refuses still votes) and its step agrees with the RCCL reference step on every rank; else the launch graph stays.
+    A wait inside the launch is bounded (DevState error kTlErrWait), so a peer that never arrives fails the check."""
+    import numpy as np
+    from simplellminference_amd import SliError
+    fits = 1
+    try:
+        model.set_exec("persist")
+    except SliError as e:
+        fits = 0
+        progress(f"persistent layers do not fit this rank's shard: {e}")
+    flag = torch.tensor([fits], dtype=torch.int32)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    all_fit = flag.item() == 1
+    if all_fit:
+        model.step()
+        got = model.logits()[0]
+        ok = bool(model.state()["error"] == 0 and np.isfinite(got).all() and np.abs(got - ref).max() <= 1e-3)
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if flag.item() == 1:
+            return "persist (one launch per rank for the layer stack; validated against rccl on every rank)"
+    if forced:
+        raise SystemExit("--tp-exec persist: the persistent layer stack does not fit or disagrees with RCCL")
+    model.set_exec("launches")
+    for b in range(B):  # clears a timed-out wait's device error flag
+        model.set_state_seq(b, (1234 + 17 * b) % model.config.vocab_size, model.config.max_length - 1, advance=False)
+    return "launches (persistent layers " + ("failed validation)" if all_fit else "do not fit every rank)")
+
+
 class StepMarks:
     """HIP events recorded on the engine stream between the timed loop's graph replays. Recording is an
     enqueue (no host wait), so the timed loop keeps its host cadence; the durations are read after the
@@ -294,7 +329,7 @@ def main():
                        device=local, seed=1, batch=B).init()
     model.fill_kv_synthetic(7, a.ctx - 1)
     for b in range(B):  # every sequence at position ctx-1 (KV rows 0..ctx-2 resident), its own token
-        model.set_state_seq(b, 1234 + 17 * b, a.ctx - 1, advance=False)
+        model.set_state_seq(b, (1234 + 17 * b) % model.config.vocab_size, a.ctx - 1, advance=False)
 
     def barrier():
         model.sync()
@@ -303,6 +338,7 @@ def main():
             dist.barrier()
 
     allreduce = "none"
+    exec_mode = "launches"
     if dist_on:
         allreduce = "rccl"
         # auto: the exchange inside wo / down per workgroup (batch 1: the GEMV; batch > 1: per MFMA group) when
@@ -316,6 +352,10 @@ def main():
             tp.open_oneshot(model)
             model.set_allreduce(os_mode)
             allreduce = f"{os_mode} (SLI_DEBUG_NOCOMM: not validated against rccl)"
+            if os_mode == "fused_wg" and a.tp_exec != "launches":  # rehearsal: persist held to the fused_wg step
+                model.step()
+                exec_mode = _try_persist(model, dist, torch, model.logits()[0].copy(), a.tp_exec == "persist", B)
+                exec_mode = exec_mode.replace("against rccl", "against the fused_wg launch graph (SLI_DEBUG_NOCOMM)")
         elif a.tp_allreduce != "rccl" and not _oneshot_opened(model, dist, torch, a.tp_allreduce):
             allreduce = "rccl (one-shot buffers could not be mapped on every rank)"
         elif a.tp_allreduce != "rccl":
@@ -330,12 +370,14 @@ def main():
             dist.all_reduce(flag, op=dist.ReduceOp.MIN)
             if flag.item() == 1:
                 allreduce = f"{os_mode} (validated against rccl on every rank)"
+                if os_mode == "fused_wg" and a.tp_exec != "launches":
+                    exec_mode = _try_persist(model, dist, torch, ref, a.tp_exec == "persist", B)
             elif a.tp_allreduce in ("oneshot", "fused", "fused_wg"):
                 raise SystemExit("one-shot all-reduce disagrees with RCCL")
             else:
                 model.set_allreduce("rccl")
                 for b in range(B):  # clears a timed-out one-shot's device error flag
-                    model.set_state_seq(b, 1234 + 17 * b, a.ctx - 1, advance=False)
+                    model.set_state_seq(b, (1234 + 17 * b) % model.config.vocab_size, a.ctx - 1, advance=False)
                 allreduce = "rccl (one-shot validation failed)"
     progress("model ready, timing the step")
     def elapsed_max(v):
@@ -383,7 +425,7 @@ def main():
     progress("greedy run")
     g_steps = min(a.greedy_steps, a.ctx - 1)
     for b in range(B):
-        model.set_state_seq(b, 1234 + 17 * b, a.ctx - 1 - g_steps, advance=True)
+        model.set_state_seq(b, (1234 + 17 * b) % model.config.vocab_size, a.ctx - 1 - g_steps, advance=True)
     barrier()
     tg = time.perf_counter()
     for _ in range(g_steps):
@@ -432,7 +474,7 @@ def main():
                    "step_bytes_per_gpu": round(wbytes + kvbytes),
                    "hbm_roofline_tokens_per_s": round(B * HBM_PEAK_GBS * 1e9 / (wbytes + kvbytes), 1),
                    "step_frac_of_hbm_peak": round((wbytes + kvbytes) / (ms * 1e-3) / (HBM_PEAK_GBS * 1e9), 4)},
-        "exec": "launches",
+        "exec": exec_mode,
         "tp_allreduce": allreduce,
         "qkv_attn_fused": model.fused_qkv_attn(),
         "roofline": {"bound": "hbm", "kernel": f"{dom}: {FAMILY_KERNELS[B > 1][dom]}",

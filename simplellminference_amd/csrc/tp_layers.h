@@ -354,14 +354,20 @@ __device__ __forceinline__ void tl_consume(const TlChunk<CH>& c, int K, int nr, 
 // over its groups in group order by one wave (deterministic).
 template <int CH, bool FIXED, class RowF>
 __device__ __forceinline__ void tl_gemv(TlSmem& sm, TlChunk<CH>& c, const __half* W, int K, int nr, const RowF& row,
-                                        const float* nw = nullptr, float scale = 1.0f) {
+                                        const float* nw = nullptr, float scale = 1.0f, const TlArgs* sa = nullptr, int lay = 0) {
     const int G = K >> 3, nch = (nr * G + CH * kTlThreads - 1) / (CH * kTlThreads);
 #pragma nounroll
     for (int ch = 0; ch < nch; ++ch) {
         if (ch > 0) tl_issue<CH, FIXED>(c, W, K, nr, row, ch);
         tl_consume<CH, FIXED>(c, K, nr, sm.xs, sm.part, ch, nw);
     }
+#ifdef TL_STAMPS
+    if (sa) { const TlArgs& a = *sa; TL_STAMPL(lay, 13); }
+#endif
     __syncthreads();
+#ifdef TL_STAMPS
+    if (sa) { const TlArgs& a = *sa; TL_STAMPL(lay, 19); }
+#endif
     const int lane = tl_tid() & 63, wave = tl_tid() >> 6;
     for (int i = wave; i < nr; i += kTlWaves) {
         float s = 0.0f;
@@ -423,9 +429,8 @@ __device__ __forceinline__ void tl_exchange(TlSmem& sm, unsigned& vp, const TlAr
                                     : tl_uniform(a.xg[p]) + ((size_t)region * 8 + a.rank) * D;
             tl_put(dst, r0 + t, v, tag);
         }
-        // the pushes acknowledged before this workgroup's first poll of its own slots, so that poll is not wasted on
-        // its own stores still in flight (uncached memory: each poll is a full memory round trip)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // (no wait for the pushes' acknowledgement before the first poll: the tags tell a value that has not landed,
+        // and waiting cost 0.3 us per layer in tools/tl_lab)
     }
     // this workgroup's rows of every rank's slot in its own buffer, summed in rank order
     float* got = sm.part;  // [nranks][nrow], one sweep over every slot
@@ -728,13 +733,15 @@ __global__ void __launch_bounds__(kTlThreads) tp_layers_kernel(TlArgs a) {
         tl_exchange(sm, vp, a, r0, nrow, 0, tb + 7);
         if (t < nrow) tl_put(a.g_x1, r0 + t, sm.xres[t], tb + 5);
         // ---- E4 -> RMSNorm -> gate/up -> SwiGLU (swiglu_kernel.cpp:12-13: sigmoid(gate) * up; act_mode 1: SiLU)
+        // (issued after the exchange and the x1 publish, never before: a store queued behind a CU's 88 KB weight share
+        // reaches its readers that much later — 1.3-1.6 us per layer in tools/tl_lab)
         TlChunk<kTlCHG> cg;
         tl_issue<kTlCHG, true>(cg, W[2], D, 2 * ng, row_gu, 0);
         tl_issue_norm(nw, a.norms + (size_t)(2 * l + 1) * D, D);
         float ss1 = 0.0f;
         tl_gather<true>(sm, vp, a.g_x1, D, tb + 5, sm.xs, a.st, &ss1);
         TL_STAMP(5);
-        tl_gemv<kTlCHG, true>(sm, cg, W[2], D, 2 * ng, row_gu, nw.w, tl_rms_inv(ss1, D, a.eps));
+        tl_gemv<kTlCHG, true>(sm, cg, W[2], D, 2 * ng, row_gu, nw.w, tl_rms_inv(ss1, D, a.eps), &a, l);
         TL_STAMP(6);
         if (t < ng) {
             const float g = sm.rows[2 * t], up = sm.rows[2 * t + 1];

@@ -4,6 +4,7 @@
 // arithmetic to the oracle, tests/test_gpu_tp_layers.py).
 //
 //   tl_lab [-m 0|1|2] [-L layers] [-r reps] [-n ranks] [-w workgroups]
+//     -x 0|1|2: the loopback exchange buffer uncached (the engine's) / plain / fine-grained
 //     -m 0: one rank (x += projection), 1: no-comm debug (the local partial), 2: the granule exchange in loopback
 //           (every slot of the rank's own uncached buffer, as SLI_DEBUG_OS_LOOPBACK), -n ranks (default 8)
 // Prints the launch time per layer and the median per-phase spans (us) of a few workgroups.
@@ -43,13 +44,14 @@ __global__ void fill_float(float* p, size_t n, float v) {
 }
 
 int main(int argc, char** argv) {
-    int mode = 1, L = 32, reps = 20, nranks = 8, nwg = 0;
+    int mode = 1, L = 32, reps = 20, nranks = 8, nwg = 0, xmem = 0;
     for (int i = 1; i + 1 < argc; i += 2) {
         if (!strcmp(argv[i], "-m")) mode = atoi(argv[i + 1]);
         if (!strcmp(argv[i], "-L")) L = atoi(argv[i + 1]);
         if (!strcmp(argv[i], "-r")) reps = atoi(argv[i + 1]);
         if (!strcmp(argv[i], "-n")) nranks = atoi(argv[i + 1]);
         if (!strcmp(argv[i], "-w")) nwg = atoi(argv[i + 1]);
+        if (!strcmp(argv[i], "-x")) xmem = atoi(argv[i + 1]);
     }
     hipDeviceProp_t prop;
     CK(hipGetDeviceProperties(&prop, 0));
@@ -106,7 +108,12 @@ int main(int argc, char** argv) {
     a.mode = mode, a.rank = nranks - 1, a.nranks = mode == 2 ? nranks : 1, a.loopback = 1;
     if (mode == 2) {
         tl_u2* buf;
-        CK(hipExtMallocWithFlags((void**)&buf, 8ull * 2 * 8 * D, hipDeviceMallocUncached));
+        // -x 0: uncached (what the engine maps over IPC), 1: plain device memory, 2: fine-grained
+        if (xmem == 1)
+            CK(hipMalloc((void**)&buf, 8ull * 2 * 8 * D));
+        else
+            CK(hipExtMallocWithFlags((void**)&buf, 8ull * 2 * 8 * D,
+                                     xmem == 2 ? hipDeviceMallocFinegrained : hipDeviceMallocUncached));
         CK(hipMemset(buf, 0, 8ull * 2 * 8 * D));
         std::vector<tl_u2*> xg(nranks, buf);
         tl_u2** xgd = (tl_u2**)dalloc(sizeof(void*) * nranks);
@@ -131,8 +138,8 @@ int main(int argc, char** argv) {
     }
     CK(hipMemcpy(&hs, st, sizeof(hs), hipMemcpyDeviceToHost));
     std::sort(ms.begin(), ms.end());
-    printf("tl_lab mode %d%s, %d layers, %d workgroups: median launch %.1f us = %.2f us per layer (device error %d)\n",
-           mode, mode == 2 ? " (loopback exchange)" : "", L, nwg, ms[reps / 2] * 1e3, ms[reps / 2] * 1e3 / L, hs.error);
+    printf("tl_lab -x %d mode %d%s, %d layers, %d workgroups: median launch %.1f us = %.2f us per layer (device error %d)\n",
+           xmem, mode, mode == 2 ? " (loopback exchange)" : "", L, nwg, ms[reps / 2] * 1e3, ms[reps / 2] * 1e3 / L, hs.error);
 #ifdef TL_STAMPS
     std::vector<unsigned long long> h(8ull * nwg * L * kTlStamps / 8);
     CK(hipMemcpy(h.data(), a.stamps, 8ull * nwg * L * kTlStamps, hipMemcpyDeviceToHost));
@@ -152,6 +159,7 @@ int main(int argc, char** argv) {
                "merge-gather %.2f merge %.2f]\n", wg,
                med(wg, 0, 14), med(wg, 14, 15), med(wg, 15, 1), med(wg, 1, 10), med(wg, 10, 11), med(wg, 10, 16),
                med(wg, 16, 17), med(wg, 17, 18), med(wg, 18, 11), med(wg, 11, 12), med(wg, 12, 2));
+        printf("  wg %3d: gu: [consume %.2f barrier %.2f reduce+act %.2f]\n", wg, med(wg, 5, 13), med(wg, 13, 19), med(wg, 19, 6));
         printf("  wg %3d:", wg);
         for (int k = 0; k < 10; ++k) {
             std::vector<double> v;
