@@ -507,6 +507,10 @@ def main():
         "settle": {**settle, "note": "untimed replays before the --warmup steps (--settle-ms)"},
     }
     out["greedy_64"]["timed_mean_over_greedy"] = round(ms / greedy["ms_per_step"], 4)
+    if exec_mode.startswith("persist"):
+        out["roofline"]["families_note"] = ("the launch graph's kernels by family (sli_model_time_families), probed beside "
+                                            "the step: the timed step ran the layer stack as ONE persistent launch per "
+                                            "rank (tp_layers_kernel), so these are the fallback path's launches")
     if B > 1:  # MFMA work of the batched projections: 2 flop per weight per sequence
         wb_el = {"f16": 2.0, "i8": 1.0, "f32": 4.0}[a.w_dtype]
         proj = [f for f in fam if f != "attention"]
