@@ -83,7 +83,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample budget")
     ap.add_argument("--gemv-iters", type=int, default=20)
     ap.add_argument("--traffic-json", default=next(
-        (p for p in (os.path.join(ROOT, "profiles", f) for f in ("r5_gemv_traffic.json", "r4_gemv_traffic.json",
+        (p for p in (os.path.join(ROOT, "profiles", f) for f in ("r6_gemv_traffic.json", "r5_gemv_traffic.json", "r4_gemv_traffic.json",
                                                                    "r3_gemv_traffic.json"))
          if os.path.exists(p)), os.path.join(ROOT, "profiles", "r5_gemv_traffic.json")))
     return ap.parse_args()
