@@ -189,13 +189,15 @@ static void attn_mfma_go(const AttnArgs<__half>& a, int blocks, int nbuf, hipStr
 // merge: the same result in out).
 template <int HD>
 static int attn_mfma_launch(AttnArgs<__half> a, int g, int T, hipStream_t s) {
-    const int tpw = attn_mfma_tpw(a.n_kv_heads, T, device_cus());
+    // the partial buffer (mha_part_bytes) holds ceil(T / pf) splits per head, pf = the fp32 kernel's positions per
+    // workgroup; at head_dim 64 that is 256 keys, so one tile per wave (128 keys) over a longer context would store
+    // past it (the round-5 fault record): the split is never shorter than pf
+    const int pf = attn_wg_positions(SLI_DT_F32, HD);
+    const int tpw = std::max(attn_mfma_tpw(a.n_kv_heads, T, device_cus()), (pf + kAmWgKeys - 1) / kAmWgKeys);
     a.ppwg = kAmWgKeys * tpw;
     a.max_splits = (T + a.ppwg - 1) / a.ppwg;
     if (a.max_splits > kAttnMaxWgSplits) return fail(SLI_ERR_SHAPE, "mha: context too long for the split merge");
-    // the partial buffer (mha_part_bytes) holds the splits of the finest geometry, the fp32 cache's; a finer split
-    // here would store past it (the round-5 fault record)
-    if (a.ppwg < attn_wg_positions(SLI_DT_F32, HD)) return fail(SLI_ERR_SHAPE, "mha: split finer than the partial buffer");
+    if (a.max_splits > (T + pf - 1) / pf) return fail(SLI_ERR_SHAPE, "mha: more splits than the partial buffer holds");
     if (a.defer_merge == 2) a.defer_merge = 0;
     const int blocks = a.n_kv_heads * a.max_splits, nbuf = tpw > 1 ? 2 : 1;
     switch (g) {

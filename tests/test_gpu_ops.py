@@ -136,7 +136,11 @@ def test_softmax(gpu, oracle, n):
                                                  # of 4 / 3 / 1 live tiles; the round-5 lab mismatches
                                                  # appeared exactly past the refill, under a full context
                                                  (16384, 128, 32, 8, 1, 16383), (16384, 128, 32, 8, 0, 16383 - 700),
-                                                 (16384, 128, 32, 8, 1, 511 + 96)])
+                                                 (16384, 128, 32, 8, 1, 511 + 96),
+                                                 # fp16 hd 64 over 1024 keys, 2 kv heads: the MFMA rule's one tile per
+                                                 # wave would give 8 splits of 128 keys against 4 in the partial buffer
+                                                 # (sized for the fp32 kernel's 256); the launch now splits at >= 256
+                                                 (1024, 64, 16, 2, 1, 1023), (1024, 64, 16, 2, 0, 300)])
 def test_mha(gpu, oracle, kv_dtype, T, hd, H, Hkv, layer, pos):
     torch = gpu
     from simplellminference_amd import ops

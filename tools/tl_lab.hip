@@ -159,7 +159,6 @@ int main(int argc, char** argv) {
                "merge-gather %.2f merge %.2f]\n", wg,
                med(wg, 0, 14), med(wg, 14, 15), med(wg, 15, 1), med(wg, 1, 10), med(wg, 10, 11), med(wg, 10, 16),
                med(wg, 16, 17), med(wg, 17, 18), med(wg, 18, 11), med(wg, 11, 12), med(wg, 12, 2));
-        printf("  wg %3d: gu: [consume %.2f barrier %.2f reduce+act %.2f]\n", wg, med(wg, 5, 13), med(wg, 13, 19), med(wg, 19, 6));
         printf("  wg %3d:", wg);
         for (int k = 0; k < 10; ++k) {
             std::vector<double> v;
