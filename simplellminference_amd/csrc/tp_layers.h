@@ -239,34 +239,6 @@ __device__ __forceinline__ void tl_gather2(TlSmem& sm, unsigned& vp, const tl_u2
     }
 }
 
-// nblk blocks of `inner` granules, `stride` apart, into dst[0 .. nblk inner) contiguous; KPER granules per thread in
-// ONE sweep (n <= KPER * 512), branch-free like tl_gather (offsets computed once per call)
-template <int KPER>
-__device__ __forceinline__ void tl_gather_blocks(TlSmem& sm, unsigned& vp, const tl_u2* g, int nblk, int inner, int stride,
-                                                 unsigned tag, float* dst, DevState* st) {
-    if (sm.dead) return;
-    const int n = nblk * inner;
-    if (n <= 0) return;
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<tl_u2*>(g), 0, 0x7fffffff, 0x00020000);
-    // (offsets recomputed every pass: held across the loop they would cost 2 KPER VGPRs)
-    for (unsigned pass = 0;; ++pass) {
-        tl_u2 v[KPER];
-#pragma unroll
-        for (int j = 0; j < KPER; ++j) {
-            const int i = min(tl_tid() + j * kTlThreads, n - 1), b = i / inner;
-            v[j] = __builtin_amdgcn_raw_buffer_load_b64(rs, 8u * (unsigned)(b * stride + (i - b * inner)), 0, 16 /* sc1 */);
-        }
-        bool miss = false;
-#pragma unroll
-        for (int j = 0; j < KPER; ++j) {
-            miss |= v[j].y != tag;
-            dst[min(tl_tid() + j * kTlThreads, n - 1)] = __uint_as_float(v[j].x);
-        }
-        if (!tl_any(sm, vp, miss)) break;
-        if (tl_give_up(sm, vp, st, pass)) return;
-    }
-}
-
 // ---------------------------------------------------------------- register-chunk GEMV over LDS-staged input
 // An op's rows on this workgroup: nr rows of K columns (K % 8 == 0), row(i) their matrix rows. Vector v of the
 // flat (row, 8-column group) sequence: row v / G, group v % G (G = K / 8); thread t holds v = (c kTlCH + j) 512 + t
@@ -742,49 +714,14 @@ __global__ void __launch_bounds__(kTlThreads) tp_layers_kernel(TlArgs a) {
             tl_attend<G>(sm, a, kv, kvh, s, S, pos, tb + 3, l);
             TL_STAMP(11);
         }
-#ifdef TL_MERGE_LOCAL
-        // every workgroup merges every head's split partials itself (no merge edge; they fit the LDS buffer, one head's
-        // splits one sweep of TL_ML_KPER granules per thread)
-#ifndef TL_ML_KPER
-#define TL_ML_KPER 9
-#endif
-        const bool merge_local = hq * ns * kTlPart <= kTlPartMax && ns * kTlPart <= TL_ML_KPER * kTlThreads;
-#else
-        constexpr bool merge_local = false;
-#endif
-        if (!merge_local)
-            for (int it = w; it < n_items; it += nwg)
-                if (it % S == 0) tl_merge<G>(sm, vp, a, it / S, S, ns, tb + 3, tb + 4, l);
+        // (merging in every workgroup instead, no merge edge: +1.3 us per layer, profiles/r6_tl_lab_ab_merge.txt)
+        for (int it = w; it < n_items; it += nwg)
+            if (it % S == 0) tl_merge<G>(sm, vp, a, it / S, S, ns, tb + 3, tb + 4, l);
         TL_STAMP(2);
         // ---- wo (+ residual, exchange)
         TlChunk<kTlCHO> co;
         tl_issue<kTlCHO, true>(co, W[1], hq * kTlHD, nrow, row_x, 0);
-        if (merge_local) {
-#ifdef TL_MERGE_LOCAL
-            {
-                const int hc = max(1, (TL_ML_KPER * kTlThreads) / (ns * kTlPart));  // heads per sweep
-                for (int h0 = 0; h0 < hq; h0 += hc)
-                    tl_gather_blocks<TL_ML_KPER>(sm, vp, a.g_part + (size_t)h0 * S * kTlPart, min(hc, hq - h0), ns * kTlPart,
-                                                 S * kTlPart, tb + 3, sm.part + (size_t)h0 * ns * kTlPart, a.st);
-            }
-            for (int i = tl_tid(); i < hq * kTlHD; i += kTlThreads) {  // attn_merge's arithmetic, splits in order
-                const int h = i / kTlHD, d = i - h * kTlHD;
-                const float* ph = sm.part + (size_t)h * ns * kTlPart;
-                float M = -INFINITY;
-                for (int s2 = 0; s2 < ns; ++s2) M = fmaxf(M, ph[s2 * kTlPart + kTlHD]);
-                float num = 0.0f, den = 0.0f;
-                for (int s2 = 0; s2 < ns; ++s2) {
-                    const float wgt = expf(ph[s2 * kTlPart + kTlHD] - M);
-                    num = fmaf(wgt, ph[s2 * kTlPart + d], num);
-                    den = fmaf(wgt, ph[s2 * kTlPart + kTlHD + 1], den);
-                }
-                sm.xs[i] = num / den;
-            }
-            __syncthreads();
-#endif
-        } else {
-            tl_gather(sm, vp, a.g_att, hq * kTlHD, tb + 4, sm.xs, a.st);
-        }
+        tl_gather(sm, vp, a.g_att, hq * kTlHD, tb + 4, sm.xs, a.st);
         TL_STAMP(3);
         tl_gemv<kTlCHO, true>(sm, co, W[1], hq * kTlHD, nrow, row_x);
         TL_STAMP(4);
