@@ -270,7 +270,7 @@ __device__ __forceinline__ void tl_vec_next(TlVec& p, int G, int q512, int r512)
 // FIXED: K / 8 divides the 512 threads (K a power of two <= 4096: q/k/v, wo and gate/up at the supported shapes), so a
 // thread's column group is fixed and the row advances by a constant; otherwise (down: K = the local FFN width) the
 // (row, group) pair is stepped incrementally
-template <int CH, bool FIXED, class RowF, int J0 = 0, int J1 = CH>
+template <int CH, bool FIXED, class RowF>
 __device__ __forceinline__ void tl_issue(TlChunk<CH>& c, const __half* W, int K, int nr, const RowF& row, int chunk) {
     const int G = K >> 3;
     if (nr <= 0) return;
@@ -280,7 +280,7 @@ __device__ __forceinline__ void tl_issue(TlChunk<CH>& c, const __half* W, int K,
     if constexpr (FIXED) {
         const int per = kTlThreads / G, g = tid % G, r0 = chunk * CH * per + tid / G;
 #pragma unroll
-        for (int j = J0; j < J1; ++j) {
+        for (int j = 0; j < CH; ++j) {
             const int r = min(r0 + j * per, nr - 1);  // clamped: a duplicate of a vector in flight, never a branch
             c.w[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, 2u * ((unsigned)row(r) * (unsigned)K + 8u * (unsigned)g), 0,
                                                            2 /* nt: streamed once */);
@@ -662,9 +662,7 @@ __global__ void __launch_bounds__(kTlThreads) tp_layers_kernel(TlArgs a) {
         }
         TlKV kv;
         const bool attn_item = w < n_items && (w % S) < ns;  // (first item only in registers early)
-#ifndef TL_KV_LATE
-        if (attn_item) tl_issue_kv(kv, a, l, w / S, w % S, pos);
-#endif
+        if (attn_item) tl_issue_kv(kv, a, l, w / S, w % S, pos);  // (after E1 instead: +0.2-0.5 us per layer)
         float ss = 0.0f;  // sum of squares of x (RMSNorm)
         if (l == 0) {  // the embedding's x, written before this launch
             float sq = 0.0f;
@@ -679,9 +677,6 @@ __global__ void __launch_bounds__(kTlThreads) tp_layers_kernel(TlArgs a) {
             tl_gather<true>(sm, vp, a.g_x, D, tb + 1, sm.xs, a.st, &ss);
         }
         TL_STAMP(0);
-#ifdef TL_KV_LATE
-        if (attn_item) tl_issue_kv(kv, a, l, w / S, w % S, pos);
-#endif
         if (t < nrow) sm.xres[t] = sm.xs[r0 + t];
         TL_STAMP(14);
         tl_gemv<kTlCHQ, true>(sm, c, W[0], D, 2 * nq, row_qkv, nw.w, tl_rms_inv(ss, D, a.eps));
@@ -736,17 +731,11 @@ __global__ void __launch_bounds__(kTlThreads) tp_layers_kernel(TlArgs a) {
         // (issued after the exchange and the x1 publish, never before: a store queued behind a CU's 88 KB weight share
         // reaches its readers that much later — 1.3-1.6 us per layer in tools/tl_lab)
         TlChunk<kTlCHG> cg;
-#ifdef TL_GU_SPLIT
-        tl_issue<kTlCHG, true, decltype(row_gu), 0, TL_GU_SPLIT>(cg, W[2], D, 2 * ng, row_gu, 0);
-#else
-        tl_issue<kTlCHG, true>(cg, W[2], D, 2 * ng, row_gu, 0);
-#endif
+        tl_issue<kTlCHG, true>(cg, W[2], D, 2 * ng, row_gu, 0);  // (half of it after E4 instead: no change)
         tl_issue_norm(nw, a.norms + (size_t)(2 * l + 1) * D, D);
         float ss1 = 0.0f;
         tl_gather<true>(sm, vp, a.g_x1, D, tb + 5, sm.xs, a.st, &ss1);
-#ifdef TL_GU_SPLIT
-        tl_issue<kTlCHG, true, decltype(row_gu), TL_GU_SPLIT, kTlCHG>(cg, W[2], D, 2 * ng, row_gu, 0);
-#endif
+
         TL_STAMP(5);
         tl_gemv<kTlCHG, true>(sm, cg, W[2], D, 2 * ng, row_gu, nw.w, tl_rms_inv(ss1, D, a.eps));
         TL_STAMP(6);
