@@ -214,15 +214,20 @@ __global__ void __launch_bounds__(kBgThreads) bgemm_kernel(const __half* __restr
     const int wq = lane & 3, wbo = (lane >> 2) & 1;  // per-wave staging: 8-k group, block offset
     float4 xa[kBgNH][2];
     float4 wn[NORM ? kBgNH : 1][2];
+#ifdef BG_LAB_NOSTAGE  // tools/bgemm_lab only: no activation loads (an upper bound on what a ready image saves)
+    constexpr bool kStage = false;
+#else
+    constexpr bool kStage = true;
+#endif
 #pragma unroll
     for (int n = 0; n < kBgNH; ++n) {
         const int blk = wb0 + max(min(2 * n + wbo, wnb - 1), 0);  // clamped into the row, never a branch
         const int k8 = min(blk, nkb - 1) * 4 + wq;
         const float4* xp = reinterpret_cast<const float4*>(in.x + (size_t)sbc * K + (size_t)k8 * 8);
-        xa[n][0] = xp[0];
-        xa[n][1] = xp[1];
+        xa[n][0] = kStage ? xp[0] : make_float4(0.f, 0.f, 0.f, 0.f);
+        xa[n][1] = kStage ? xp[1] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    if constexpr (NORM) {
+    if constexpr (NORM && kStage) {
 #pragma unroll
         for (int n = 0; n < kBgNH; ++n) {
             const int blk = wb0 + max(min(2 * n + wbo, wnb - 1), 0);
