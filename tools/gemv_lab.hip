@@ -151,6 +151,60 @@ __global__ void __launch_bounds__(1024) stream_dyn_kernel(const char* p, long lo
     if (acc == 1.2345f) out[blockIdx.x] = acc;
 }
 
+// streaming read with a WAVE-level dynamic tail (round 6, mode "dyn2"): the work is cut into units of U KiB (one
+// 16-byte load per lane x U); the first static_frac of the units is split evenly over the grid's waves (contiguous
+// per wave), the rest into 8 per-XCD pools (pool x = units [S + x D / 8, S + (x + 1) D / 8), x = HW_REG_XCC_ID) that
+// the XCD's waves drain one unit per ticket: lane 0 adds 1 to the XCD's head (agent scope) and the next ticket is
+// requested with the current unit's loads, so the hand-out round trip hides under the unit. No workgroup barrier.
+// ctr: 8 heads 128 B apart, zero before the launch. (Round 5's dyn took 128-KiB chunks per WORKGROUP from one
+// counter behind a barrier: a chunk was ~5 us of a CU's stream, coarser than the tail it was meant to remove.)
+template <int U>
+__global__ void __launch_bounds__(1024) stream_dyn2_kernel(const char* p, long long bytes, float* out, unsigned* ctr,
+                                                           float static_frac, unsigned long long* st = nullptr) {
+    const unsigned long long t0 = st ? __builtin_amdgcn_s_memrealtime() : 0;
+    const int lane = threadIdx.x & 63;
+    const int gw = blockIdx.x * 16 + __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), nw = gridDim.x * 16;
+    const long long ub = 1024LL * U;
+    const int nu = (int)(bytes / ub);
+    const int ns = (int)(nu * static_frac);
+    const int u1 = (int)((long long)(gw + 1) * ns / nw);
+    int u = (int)((long long)gw * ns / nw);
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    xcc &= 7;
+    const int nd = nu - ns;
+    const int d0 = ns + (int)((long long)xcc * nd / 8), dn = ns + (int)((long long)(xcc + 1) * nd / 8) - d0;
+    unsigned* head = ctr + xcc * 32;
+    unsigned tk = 0;
+    if (lane == 0) tk = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    float acc = 0.0f;
+    for (;;) {
+        int unit;
+        if (u < u1) {
+            unit = u++;
+        } else {
+            const int t = __builtin_amdgcn_readfirstlane((int)tk);
+            if (t >= dn) break;
+            unit = d0 + t;
+            if (lane == 0) tk = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const char* b = p + (size_t)unit * ub + lane * 16;
+        u32x4 w[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) w[j] = load16<true>(b + j * 1024);
+#pragma unroll
+        for (int j = 0; j < U; ++j) acc += __uint_as_float(w[j].x ^ w[j].y ^ w[j].z ^ w[j].w);
+    }
+    if (acc == 1.2345f) out[blockIdx.x] = acc;
+    if (st && lane == 0) {
+        unsigned long long* q = st + ((size_t)blockIdx.x * 16 + (threadIdx.x >> 6)) * 4;
+        q[0] = t0;
+        q[1] = t0 + 1000000000ull * xcc;
+        q[2] = __builtin_amdgcn_s_memrealtime();
+        q[3] = 1;
+    }
+}
+
 // latency probe: wave 0 times one L2-hot load while the other 15 waves of the CU have `nw` 16-byte HBM
 // loads per lane in flight (nw = 0: idle CU). scalar = 1: wave 0 uses a scalar (s_load) read instead.
 __global__ void __launch_bounds__(1024) probe_kernel(const char* W, const float* x, int nw, int scalar,
@@ -292,6 +346,44 @@ int main(int argc, char** argv) {
             DMA_CFG("dma def S8 1024t", 8, false, 1024)
             DMA_CFG("dma def S32 256t", 32, false, 256)
 #undef DMA_CFG
+        }
+        return 0;
+    }
+    if (mode == "dyn2") {
+        // static stream floor (stream_kernel<8>) vs the wave-level dynamic tail (stream_dyn2_kernel) at unit sizes
+        // 4 / 8 KiB and static fractions 0.5-0.95; NL distinct matrices per shape in a graph, a memset zeroing the
+        // per-XCD heads first (in both, so the floor pays the same node)
+        unsigned* ctr;
+        CK(hipMalloc(&ctr, NL * 8 * 128));
+        for (int si : {0, 1, 2, 3}) {
+            const long long bytes = (long long)kShapes[si].rows * kShapes[si].cols * 2;
+            auto rep = [&](const char* name, const std::function<void(int)>& f) {
+                for (int r = 0; r < 2; ++r) {
+                    const float ms = time_graph(s, [&] {
+                        CK(hipMemsetAsync(ctr, 0, NL * 8 * 128, s));
+                        for (int l = 0; l < NL; ++l) f(l);
+                    });
+                    const double us = 1000.0 * ms / NL;
+                    printf("%-5s %-26s %7.2f us  %7.1f GB/s\n", kShapes[si].name, name, us, bytes / (us * 1e-6) / 1e9);
+                }
+                fflush(stdout);
+            };
+            rep("static reg 8x16B", [&](int l) {
+                hipLaunchKernelGGL(stream_kernel<8>, dim3(256), dim3(1024), 0, s, (const char*)w[si][l], bytes, y2, nullptr);
+            });
+            for (float fr : {0.95f, 0.9f, 0.8f, 0.5f}) {
+                char nm[64];
+                snprintf(nm, sizeof nm, "dyn2 U8 static %.2f", fr);
+                rep(nm, [&](int l) {
+                    hipLaunchKernelGGL(stream_dyn2_kernel<8>, dim3(256), dim3(1024), 0, s, (const char*)w[si][l], bytes, y2,
+                                       ctr + l * 8 * 32, fr, nullptr);
+                });
+                snprintf(nm, sizeof nm, "dyn2 U4 static %.2f", fr);
+                rep(nm, [&](int l) {
+                    hipLaunchKernelGGL(stream_dyn2_kernel<4>, dim3(256), dim3(1024), 0, s, (const char*)w[si][l], bytes, y2,
+                                       ctr + l * 8 * 32, fr, nullptr);
+                });
+            }
         }
         return 0;
     }

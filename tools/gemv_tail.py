@@ -45,6 +45,16 @@ def main(path):
               f"(all {run[live].mean():5.2f}), steps {steps[slow].mean():6.1f} (all {steps[live].mean():6.1f})")
         print("      slowest 2% by XCD: " + " ".join(f"{x}:{int((slow & (xcd == x)).sum())}" for x in range(8))
               + " | by wave slot: " + " ".join(str(int((slow & (wslot[None, :] == w)).sum())) for w in range(16)))
+        # what balancing would leave (round 6): per launch, the last wave's exit against the slowest workgroup's MEAN
+        # wave exit (its waves sharing the workgroup's work) and the slowest XCD's mean (work shared per XCD)
+        exm = np.where(live, ex, np.nan).reshape(ex.shape[0], -1, 16)
+        end = np.nanmax(exm, axis=(1, 2))
+        wg_mean = np.nanmax(np.nanmean(exm, axis=2), axis=1)
+        xc = xcd.reshape(ex.shape[0], -1, 16)[:, :, 0]
+        xcd_mean = np.nanmax(np.stack([np.nanmean(np.where(xc[:, :, None] == x, exm, np.nan), axis=(1, 2))
+                                       for x in range(8)], axis=1), axis=1)
+        print(f"      last exit p50 {np.median(end):5.2f} | slowest workgroup's mean exit p50 {np.median(wg_mean):5.2f} | "
+              f"slowest XCD's mean exit p50 {np.median(xcd_mean):5.2f} | all-wave mean {np.nanmean(exm):5.2f} us")
 
 
 if __name__ == "__main__":
