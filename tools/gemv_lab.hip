@@ -205,6 +205,54 @@ __global__ void __launch_bounds__(1024) stream_dyn2_kernel(const char* p, long l
     }
 }
 
+// dyn2 refined (mode "dyn3"): only the first DW waves of a workgroup take dynamic units (DW x 256 pullers instead of
+// 4096), a wave requests its first ticket with its LAST static unit (not at entry, where 4096 adds queued ~6 us
+// ahead of every first weight load), and each XCD's pool is split into NP sub-pools by workgroup (fewer pullers per
+// head word; a sub-pool balances its 32 / NP CUs only).
+template <int U, int DW, int NP>
+__global__ void __launch_bounds__(1024) stream_dyn3_kernel(const char* p, long long bytes, float* out, unsigned* ctr,
+                                                           float static_frac) {
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const int gw = blockIdx.x * 16 + wv, nw = gridDim.x * 16;
+    const long long ub = 1024LL * U;
+    const int nu = (int)(bytes / ub);
+    const int ns = (int)(nu * static_frac);
+    const int u1 = (int)((long long)(gw + 1) * ns / nw);
+    int u = (int)((long long)gw * ns / nw);
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    xcc &= 7;
+    const int pool = (int)xcc * NP + (int)((blockIdx.x >> 3) % NP), npool = 8 * NP;
+    const int nd = nu - ns;
+    const int d0 = ns + (int)((long long)pool * nd / npool), dn = ns + (int)((long long)(pool + 1) * nd / npool) - d0;
+    unsigned* head = ctr + pool * 32;
+    const bool dyn = wv < DW;
+    unsigned tk = 0;
+    if (dyn && u1 <= u && lane == 0) tk = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    float acc = 0.0f;
+    for (;;) {
+        int unit;
+        if (u < u1) {
+            unit = u++;
+            if (dyn && u == u1 && lane == 0) tk = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (!dyn) break;
+            const int t = __builtin_amdgcn_readfirstlane((int)tk);
+            if (t >= dn) break;
+            unit = d0 + t;
+            if (lane == 0) tk = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const char* b = p + (size_t)unit * ub + lane * 16;
+        u32x4 w[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) w[j] = load16<true>(b + j * 1024);
+#pragma unroll
+        for (int j = 0; j < U; ++j) acc += __uint_as_float(w[j].x ^ w[j].y ^ w[j].z ^ w[j].w);
+    }
+    if (acc == 1.2345f) out[blockIdx.x] = acc;
+}
+
 // latency probe: wave 0 times one L2-hot load while the other 15 waves of the CU have `nw` 16-byte HBM
 // loads per lane in flight (nw = 0: idle CU). scalar = 1: wave 0 uses a scalar (s_load) read instead.
 __global__ void __launch_bounds__(1024) probe_kernel(const char* W, const float* x, int nw, int scalar,
@@ -346,6 +394,36 @@ int main(int argc, char** argv) {
             DMA_CFG("dma def S8 1024t", 8, false, 1024)
             DMA_CFG("dma def S32 256t", 32, false, 256)
 #undef DMA_CFG
+        }
+        return 0;
+    }
+    if (mode == "dyn3") {
+        unsigned* ctr;
+        CK(hipMalloc(&ctr, NL * 32 * 128));
+        for (int si : {0, 1, 2, 3}) {
+            const long long bytes = (long long)kShapes[si].rows * kShapes[si].cols * 2;
+            auto rep = [&](const char* name, const std::function<void(int)>& f) {
+                for (int r = 0; r < 2; ++r) {
+                    const float ms = time_graph(s, [&] {
+                        CK(hipMemsetAsync(ctr, 0, NL * 32 * 128, s));
+                        for (int l = 0; l < NL; ++l) f(l);
+                    });
+                    const double us = 1000.0 * ms / NL;
+                    printf("%-5s %-30s %7.2f us  %7.1f GB/s\n", kShapes[si].name, name, us, bytes / (us * 1e-6) / 1e9);
+                }
+                fflush(stdout);
+            };
+            rep("static reg 8x16B", [&](int l) {
+                hipLaunchKernelGGL(stream_kernel<8>, dim3(256), dim3(1024), 0, s, (const char*)w[si][l], bytes, y2, nullptr);
+            });
+#define DYN3(U_, DW_, NP_, FR)                                                                                   \
+            rep("dyn3 U" #U_ " DW" #DW_ " NP" #NP_ " static " #FR, [&](int l) {                                    \
+                hipLaunchKernelGGL((stream_dyn3_kernel<U_, DW_, NP_>), dim3(256), dim3(1024), 0, s,                  \
+                                   (const char*)w[si][l], bytes, y2, ctr + l * 32 * 32, FR##f);                      \
+            });
+            DYN3(8, 16, 1, 0.95) DYN3(8, 4, 1, 0.95) DYN3(8, 4, 4, 0.95) DYN3(8, 2, 1, 0.95)
+            DYN3(8, 4, 1, 0.9) DYN3(8, 4, 4, 0.9) DYN3(8, 16, 4, 0.9) DYN3(8, 4, 1, 0.98)
+#undef DYN3
         }
         return 0;
     }
