@@ -1042,34 +1042,43 @@ struct StepRecorder {
             return SLI_OK;
         }
     }
-    // The GEMM tiling (prefill.h PgCfg<BM, WR, S>) per weight type, projection role and chunk size: the
-    // fastest of the tools/pgemm_lab sweep (profiles/r3_pgemm_lab.txt) on the 7B shapes at a 256-row chunk.
-    // role 0: qkv, 1: gate/up, 2: wo / down (N = D: few row blocks, so small chunk blocks for a full grid)
-    template <class Epi>
-    static int pg(sli_model* m, const void* W, int N, int K, const __half* hi, const __half* lo, const Epi& e, int M,
-                  int role) {
+    // The GEMM tiling (prefill.h PgCfg<BM, WR, S, AT, PIPE>) per weight type, projection role and chunk size: the
+    // fastest of the tools/pgemm_lab sweeps on the 7B shapes (profiles/r3_pgemm_lab.txt; round 6: the pipelined
+    // fragment reads, 5-20 % faster at every tiling, the M = 128 choices, profiles/r6b_pg_pipe.txt, and the M = 256
+    // ones re-timed with the weights streamed from HBM as in the engine, profiles/r6b_pg_cold.txt).
+    // role 0: qkv, 1: gate/up, 2: wo / down (N = D: few row blocks, so small chunk blocks for a full grid).
+    // f(PgCfg<...>{}) is called with the chosen tiling (pg launches it, allow_pg sets its LDS limit).
+    template <class F>
+    static int pg_pick(int M, int role, F&& f) {
         if constexpr (std::is_same<WT, int8_t>::value) {
-            if (M == 32) return pg_cfg<Epi, PgCfg<32, 2, 4>>(m, W, N, K, hi, lo, e, M);
-            if (role == 2) return pg_cfg<Epi, PgCfg<64, 2, 2>>(m, W, N, K, hi, lo, e, M);
-            if (role == 1 || M == 64) return pg_cfg<Epi, PgCfg<64, 4, 2>>(m, W, N, K, hi, lo, e, M);
-            return pg_cfg<Epi, PgCfg<128, 4, 2>>(m, W, N, K, hi, lo, e, M);
+            if (M == 32) return f(PgCfg<32, 2, 4, 2, true>{});
+            if (role == 2) return M == 256 ? f(PgCfg<64, 2, 2, 2, true>{}) : f(PgCfg<32, 2, 4, 2, true>{});
+            if (role == 1) return M == 128 ? f(PgCfg<128, 4, 2, 2, true>{}) : f(PgCfg<64, 4, 2, 2, true>{});
+            return M == 256 ? f(PgCfg<128, 4, 2, 2, true>{}) : f(PgCfg<64, 4, 2, 2, true>{});
         } else {
-            if (M == 32 || role == 2) return pg_cfg<Epi, PgCfg<32, 2, 4>>(m, W, N, K, hi, lo, e, M);
-            if (M == 64) return pg_cfg<Epi, PgCfg<64, 2, 3>>(m, W, N, K, hi, lo, e, M);
-            return pg_cfg<Epi, PgCfg<128, 2, 2>>(m, W, N, K, hi, lo, e, M);
+            if (M == 32) return f(PgCfg<32, 2, 4, 2, true>{});
+            if (role == 2) return M == 256 ? f(PgCfg<64, 2, 3, 2, true>{}) : f(PgCfg<32, 2, 4, 2, true>{});
+            if (M == 64 || (M == 128 && role == 0)) return f(PgCfg<64, 2, 3, 2, true>{});
+            // M = 256 with the weights streamed from HBM (profiles/r6b_pg_cold.txt): 8-wave workgroups
+            // (q/k/v: the weights in a 4-deep ring of their own, profiles/r6b_pg_split.txt)
+            if (M == 256) return role == 0 ? f(PgCfg<128, 4, 2, 2, true, 4>{}) : f(PgCfg<64, 4, 3, 2, true>{});
+            return f(PgCfg<128, 2, 2, 2, true>{});
         }
     }
     template <class Epi>
+    static int pg(sli_model* m, const void* W, int N, int K, const __half* hi, const __half* lo, const Epi& e, int M,
+                  int role) {
+        return pg_pick(M, role, [&](auto cfg) { return pg_cfg<Epi, decltype(cfg)>(m, W, N, K, hi, lo, e, M); });
+    }
+    template <class Epi>
     static int allow_pg(sli_model*) {
-        if constexpr (std::is_same<WT, int8_t>::value) {
-            SLI_HIP((pgemm_allow_lds<Epi, PgCfg<32, 2, 4>, WT>()));
-            SLI_HIP((pgemm_allow_lds<Epi, PgCfg<64, 2, 2>, WT>()));
-            SLI_HIP((pgemm_allow_lds<Epi, PgCfg<64, 4, 2>, WT>()));
-            SLI_HIP((pgemm_allow_lds<Epi, PgCfg<128, 4, 2>, WT>()));
-        } else if constexpr (std::is_same<WT, __half>::value) {
-            SLI_HIP((pgemm_allow_lds<Epi, PgCfg<32, 2, 4>, WT>()));
-            SLI_HIP((pgemm_allow_lds<Epi, PgCfg<64, 2, 3>, WT>()));
-            SLI_HIP((pgemm_allow_lds<Epi, PgCfg<128, 2, 2>, WT>()));
+        if constexpr (std::is_same<WT, int8_t>::value || std::is_same<WT, __half>::value) {
+            for (int M : {32, 64, 128, 256})
+                for (int role = 0; role < 3; ++role)
+                    SLI_TRY(pg_pick(M, role, [&](auto cfg) -> int {
+                        SLI_HIP((pgemm_allow_lds<Epi, decltype(cfg), WT>()));
+                        return SLI_OK;
+                    }));
         }
         return SLI_OK;
     }

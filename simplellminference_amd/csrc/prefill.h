@@ -10,7 +10,9 @@
 //      from HBM once per BM positions (the decode step reads it once per position). Operands are staged
 //      through a 3-deep LDS ring by LDS-DMA (global_load_lds_dwordx4: one 1-KiB fragment image per
 //      wave-instruction, read back conflict-free by ds_read_b128), two k-blocks in flight behind a counted
-//      vmcnt and a raw s_barrier (cdna_hip_programming.md §5 "Pipelining across barriers"). Fused epilogues:
+//      vmcnt and a raw s_barrier (cdna_hip_programming.md §5 "Pipelining across barriers"); the fragment reads of
+//      the next k-block are issued ahead of the current k-block's MFMAs (two register sets, across the stage
+//      barrier too: PgCfg::PIPE, round 6, 5-20 % faster per GEMM, bit-identical sums). Fused epilogues:
 //      RoPE + K/V cache rows + q (model.cpp:52-67), residual add (:86-90, :124-128), SwiGLU (:111-115,
 //      written straight as the down projection's hi/lo operand);
 //   3. pf_attn_mfma_kernel (fp16 KV, the default): block-causal attention of 16 chunk rows x one head against
@@ -140,15 +142,23 @@ struct PgIn {
 // (16 rows x 16 B per lane group) stay conflict-free. S stages in the LDS ring, S - 1 of them in flight.
 // Epilogue contract: row(t, i) = weight row of 16-row tile t's row i (i < 16, always valid); store(t, i0, m, v)
 // gets the fp32 sums of tile rows i0 .. i0+3 (i0 % 4 == 0) for chunk row m.
-template <int BM_, int WR_, int S_>
+// AT_: 16-row weight tiles per wave (2: a wave's 32 rows; 4: 64 rows, so every B fragment read from LDS feeds twice
+// the MFMAs). PIPE_: the fragment reads of k-block j + 1 issued before the MFMAs of k-block j (two register sets),
+// across the stage barrier too, and every hi MFMA of a k-block ahead of its lo MFMAs (no back-to-back MFMAs on one
+// accumulator); each tile's sums are added in the same order either way (bit-identical).
+// SA_ > 0 (PIPE only): the weight (A) images get a ring of their own, SA_ stages deep (SA_ - 1 issued ahead), and
+// the activation (B) images a 2-stage ring (one ahead): the A bytes come from HBM (read once per chunk), the B bytes
+// from L2, so only A needs the deep prefetch, and B, the larger image, does not pay for it in LDS.
+template <int BM_, int WR_, int S_, int AT_ = 2, bool PIPE_ = false, int SA_ = 0>
 struct PgCfg {
-    static constexpr int BM = BM_, WR = WR_, S = S_;
+    static constexpr int BM = BM_, WR = WR_, S = S_, AT = AT_, SA = SA_;
+    static constexpr bool PIPE = PIPE_;
 };
 
 template <class Cfg, typename WT>
 struct PgGeo {
-    static constexpr int BM = Cfg::BM, WR = Cfg::WR, S = Cfg::S;
-    static constexpr int WAVES = 2 * WR, THREADS = 64 * WAVES, BN = 32 * WR;
+    static constexpr int BM = Cfg::BM, WR = Cfg::WR, S = Cfg::S, AT = Cfg::AT;
+    static constexpr int WAVES = 2 * WR, THREADS = 64 * WAVES, BN = 16 * AT * WR;
     static constexpr int KS = sizeof(WT) == 1 ? 128 : 64;  // depth per stage
     static constexpr int KBS = KS / 32;                    // MFMA k-blocks per stage
     static constexpr int A_ROW = KS * (int)sizeof(WT);     // 128 B
@@ -156,14 +166,19 @@ struct PgGeo {
     static constexpr int A_IMG = 16 * A_ROW, B_IMG = 16 * B_ROW;
     static constexpr int PT = BM / 16;  // position tiles per workgroup
     static constexpr int WPT = PT / 2;  // per wave
-    static constexpr int NA = 2 * WR;   // weight row tiles
+    static constexpr int NA = AT * WR;  // weight row tiles
     static constexpr int A_BYTES = NA * A_IMG;
     static constexpr int STAGE = A_BYTES + 2 * PT * B_IMG;
     static constexpr int NDMA = STAGE / 1024;  // wave-instructions per stage
     static constexpr int DPW = NDMA / WAVES;   // per wave
-    static constexpr size_t LDS = (size_t)S * STAGE;
+    static constexpr int SA = Cfg::SA;         // split rings (PgCfg): A pieces per wave DPA, B pieces DPB
+    static constexpr int B_BYTES = STAGE - A_BYTES;
+    static constexpr int DPA = SA ? A_BYTES / 1024 / WAVES : 0, DPB = SA ? B_BYTES / 1024 / WAVES : 0;
+    static constexpr size_t LDS = SA ? (size_t)SA * A_BYTES + (size_t)S * B_BYTES : (size_t)S * STAGE;
     static_assert(A_ROW == 128 && WPT >= 1 && NDMA % WAVES == 0, "tiling");
     static_assert(S >= 2 && (S - 1) * DPW <= 63, "ring depth (vmcnt counts 63 loads)");
+    static_assert(SA == 0 || (Cfg::PIPE && S == 2 && SA >= 2 && (A_BYTES / 1024) % WAVES == 0 &&
+                              (B_BYTES / 1024) % WAVES == 0 && (SA - 1) * DPA + DPB <= 63), "split rings");
     static_assert(LDS <= 160 * 1024, "LDS");
 };
 
@@ -233,7 +248,10 @@ __global__ void __launch_bounds__(128 * Cfg::WR) pgemm_kernel(PgIn<WT> in, Epi e
     int back[Geo::DPW];  // bytes to step back in a half last stage (logical chunk in the stage's second half)
 #pragma unroll
     for (int j = 0; j < Geo::DPW; ++j) {
-        const int off = (wave * Geo::DPW + j) * 1024;
+        // split rings: the wave's DPA pieces of the A images, then its DPB pieces of the B images
+        const int off = Geo::SA ? (j < Geo::DPA ? (wave * Geo::DPA + j) * 1024
+                                                : Geo::A_BYTES + (wave * Geo::DPB + j - Geo::DPA) * 1024)
+                                : (wave * Geo::DPW + j) * 1024;
         if (off < Geo::A_BYTES) {
             const int t = rb * Geo::NA + off / Geo::A_IMG;
             const int r = (off % Geo::A_IMG) / Geo::A_ROW + lane / 8;
@@ -259,20 +277,123 @@ __global__ void __launch_bounds__(128 * Cfg::WR) pgemm_kernel(PgIn<WT> in, Epi e
         const unsigned dst = ring + (unsigned)((s % S) * Geo::STAGE);
         const bool tail = half_tail && s == ns - 1;
 #pragma unroll
-        for (int j = 0; j < Geo::DPW; ++j)
+        for (int j = 0; j < Geo::DPW; ++j) {
+#ifdef PG_LAB_SKIP  // tools/pgemm_lab only (bit 0: no A pieces, bit 1: no B pieces): timing bounds, wrong sums
+            const bool isa = (wave * Geo::DPW + j) * 1024 < Geo::A_BYTES;
+            if (((PG_LAB_SKIP & 1) && isa) || ((PG_LAB_SKIP & 2) && !isa)) continue;
+#endif
             pf_dma(src[j] + (size_t)s * adv[j] - (tail ? back[j] : 0), dst + (unsigned)((wave * Geo::DPW + j) * 1024));
+        }
     };
 
-    pf_float4 acc[2][Geo::WPT];
+    // split rings: A stage s in slot s % SA at ring, B stage s in slot s % 2 behind the A ring
+    const unsigned ring_b = ring + (unsigned)(Geo::SA * Geo::A_BYTES);
+    auto issue_a = [&](int s) {
+        const unsigned dst = ring + (unsigned)((s % Geo::SA) * Geo::A_BYTES);
+        const bool tail = half_tail && s == ns - 1;
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+        for (int j = 0; j < Geo::DPA; ++j)
+            pf_dma(src[j] + (size_t)s * adv[j] - (tail ? back[j] : 0), dst + (unsigned)((wave * Geo::DPA + j) * 1024));
+    };
+    auto issue_b = [&](int s) {
+        const unsigned dst = ring_b + (unsigned)((s & 1) * Geo::B_BYTES);
+        const bool tail = half_tail && s == ns - 1;
+#pragma unroll
+        for (int j = 0; j < Geo::DPB; ++j)
+            pf_dma(src[Geo::DPA + j] + (size_t)s * adv[Geo::DPA + j] - (tail ? back[Geo::DPA + j] : 0),
+                   dst + (unsigned)((wave * Geo::DPB + j) * 1024));
+    };
+    constexpr int AT = Geo::AT;
+    pf_float4 acc[AT][Geo::WPT];
+#pragma unroll
+    for (int a = 0; a < AT; ++a)
 #pragma unroll
         for (int b = 0; b < Geo::WPT; ++b) acc[a][b] = pf_float4{0.0f, 0.0f, 0.0f, 0.0f};
 
     // fragment read offsets: lane l reads row / column r = l & 15, k group kg = l >> 4 of each 32-k block
     const int kg = lane >> 4, r16 = lane & 15;
     const int sa = pg_swz(r16, Geo::A_ROW), sb = pg_swz(r16, Geo::B_ROW);
-    for (int s = 0; s < S - 1 && s < ns; ++s) issue(s);
+    if constexpr (Geo::SA == 0) {
+        for (int s = 0; s < S - 1 && s < ns; ++s) issue(s);
+    } else {  // the schedule of iterations -(SA - 1) .. -1: B(i + 1), then A(i + SA - 1)
+        for (int i = 1 - Geo::SA; i < 0; ++i) {
+            if (i + 1 >= 0 && i + 1 < ns) issue_b(i + 1);
+            if (i + Geo::SA - 1 >= 0 && i + Geo::SA - 1 < ns) issue_a(i + Geo::SA - 1);
+        }
+    }
+    // fragments of k-block kb of stage buffer st (A images at st, B images at stb) into (af, bh, bl)
+    auto read_frags = [&](const char* st, const char* stb, int kb, u32x4(&af)[AT], u32x4(&bh)[Geo::WPT],
+                          u32x4(&bl)[Geo::WPT]) {
+#pragma unroll
+        for (int a = 0; a < AT; ++a) {
+            const char* img = st + (wr * AT + a) * Geo::A_IMG + r16 * Geo::A_ROW;
+            if constexpr (sizeof(WT) == 2) {
+                af[a] = *reinterpret_cast<const u32x4*>(img + ((4 * kb + kg) ^ sa) * 16);
+            } else {
+                const int off = ((2 * kb + (kg >> 1)) ^ sa) * 16 + 8 * (kg & 1);
+                af[a] = pg_i8_to_f16(*reinterpret_cast<const uint2*>(img + off));
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < Geo::WPT; ++b) {
+            const int pt = wp * Geo::WPT + b;
+            const char* img = stb + (2 * pt) * Geo::B_IMG + r16 * Geo::B_ROW + ((4 * kb + kg) ^ sb) * 16;
+            bh[b] = *reinterpret_cast<const u32x4*>(img);
+            bl[b] = *reinterpret_cast<const u32x4*>(img + Geo::B_IMG);
+        }
+    };
+    auto mfmas = [&](const u32x4(&af)[AT], const u32x4(&bh)[Geo::WPT], const u32x4(&bl)[Geo::WPT]) {
+#pragma unroll
+        for (int b = 0; b < Geo::WPT; ++b)
+#pragma unroll
+            for (int a = 0; a < AT; ++a) acc[a][b] = pf_mfma(af[a], bh[b], acc[a][b]);
+#pragma unroll
+        for (int b = 0; b < Geo::WPT; ++b)
+#pragma unroll
+            for (int a = 0; a < AT; ++a) acc[a][b] = pf_mfma(af[a], bl[b], acc[a][b]);
+    };
+    if constexpr (Cfg::PIPE) {
+        // set X holds even k-blocks, set Y odd ones (KBS is even; an int8 half stage has KBS / 2 = 2): per stage
+        // read(0) -> X, MFMA(Y: the previous stage's last k-block), read(1) -> Y, MFMA(X), ... The stage barrier
+        // follows this wave's lgkmcnt(0), so the previous stage's buffer is free for the DMA issued after it while
+        // its last fragments wait in registers.
+        static_assert(KBS % 2 == 0, "k-blocks per stage");
+        u32x4 xa[AT], xh[Geo::WPT], xl[Geo::WPT], ya[AT], yh[Geo::WPT], yl[Geo::WPT];
+        for (int s = 0; s < ns; ++s) {
+            const char *st, *stb;
+            if constexpr (Geo::SA == 0) {
+                pg_wait_stages<Geo::DPW>(min(S - 2, ns - 1 - s));
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                if (s + S - 1 < ns) issue(s + S - 1);
+                st = pg_smem + (size_t)(s % S) * Geo::STAGE;
+                stb = st + Geo::A_BYTES;
+            } else {
+                // B(s) was the first load of iteration s - 1; only that iteration's A pieces (if it issued any) were
+                // issued after it, and A(s) before it
+                if (s + Geo::SA - 2 < ns)
+                    pf_wait_vm<Geo::DPA>();
+                else
+                    pf_wait_vm<0>();
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                if (s + 1 < ns) issue_b(s + 1);
+                if (s + Geo::SA - 1 < ns) issue_a(s + Geo::SA - 1);
+                st = pg_smem + (size_t)(s % Geo::SA) * Geo::A_BYTES;
+                stb = pg_smem + (size_t)Geo::SA * Geo::A_BYTES + (size_t)(s & 1) * Geo::B_BYTES;
+            }
+            const int kbs = (half_tail && s == ns - 1) ? KBS / 2 : KBS;  // wave-uniform, even
+#pragma unroll
+            for (int kb = 0; kb < KBS; kb += 2) {
+                if (kb >= kbs) break;
+                read_frags(st, stb, kb, xa, xh, xl);
+                if (s > 0 || kb > 0) mfmas(ya, yh, yl);
+                read_frags(st, stb, kb + 1, ya, yh, yl);
+                mfmas(xa, xh, xl);
+            }
+        }
+        mfmas(ya, yh, yl);
+    } else {
     for (int s = 0; s < ns; ++s) {
         // this wave's pieces of stage s landed (stages s + 1 .. s + S - 2 may stay in flight)
         pg_wait_stages<Geo::DPW>(min(S - 2, ns - 1 - s));
@@ -283,10 +404,10 @@ __global__ void __launch_bounds__(128 * Cfg::WR) pgemm_kernel(PgIn<WT> in, Epi e
 #pragma unroll
         for (int kb = 0; kb < KBS; ++kb) {
             if (kb >= kbs) break;
-            u32x4 af[2], bh[Geo::WPT], bl[Geo::WPT];
+            u32x4 af[AT], bh[Geo::WPT], bl[Geo::WPT];
 #pragma unroll
-            for (int a = 0; a < 2; ++a) {
-                const char* img = st + (wr * 2 + a) * Geo::A_IMG + r16 * Geo::A_ROW;
+            for (int a = 0; a < AT; ++a) {
+                const char* img = st + (wr * AT + a) * Geo::A_IMG + r16 * Geo::A_ROW;
                 if constexpr (sizeof(WT) == 2) {
                     af[a] = *reinterpret_cast<const u32x4*>(img + ((4 * kb + kg) ^ sa) * 16);
                 } else {  // k 32 kb + 8 kg .. +8: chunk 2 kb + kg / 2, half kg % 2
@@ -303,19 +424,26 @@ __global__ void __launch_bounds__(128 * Cfg::WR) pgemm_kernel(PgIn<WT> in, Epi e
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-            for (int a = 0; a < 2; ++a)
+            for (int a = 0; a < AT; ++a)
 #pragma unroll
                 for (int b = 0; b < Geo::WPT; ++b) {
+#if defined(PG_LAB_MFMA) && PG_LAB_MFMA == 0  // tools/pgemm_lab only: no MFMA (data movement alone)
+                    acc[a][b][0] += __uint_as_float(af[a][0] ^ bh[b][0] ^ bl[b][0]);
+#else
                     acc[a][b] = pf_mfma(af[a], bh[b], acc[a][b]);
+#if !(defined(PG_LAB_MFMA) && PG_LAB_MFMA == 1)  // PG_LAB_MFMA 1: the hi MFMA only
                     acc[a][b] = pf_mfma(af[a], bl[b], acc[a][b]);
+#endif
+#endif
                 }
         }
+    }
     }
     // C[i][n] of a 16x16 tile: lane l holds rows 4 (l >> 4) + r, column l & 15
     const int i0 = 4 * (lane >> 4);
 #pragma unroll
-    for (int a = 0; a < 2; ++a) {
-        const int t = rb * Geo::NA + wr * 2 + a;
+    for (int a = 0; a < AT; ++a) {
+        const int t = rb * Geo::NA + wr * AT + a;
         if (t >= nt) continue;
 #pragma unroll
         for (int b = 0; b < Geo::WPT; ++b) {

@@ -35,6 +35,8 @@ struct Shape {
 template <typename WT>
 struct Bufs {
     WT* W;
+    std::vector<WT*> Wc;  // the timing loop rotates over copies (none MALL-resident: weights stream from HBM as in
+                          // the engine, where a layer's weights are read once per chunk)
     __half *hi, *lo;
     float* y;
     PfState* ps;
@@ -67,6 +69,14 @@ static void make(Bufs<WT>& b, int N, int K, int M) {
     CK(hipMalloc(&b.y, sizeof(float) * (size_t)M * N));
     CK(hipMalloc(&b.ps, sizeof(PfState)));
     CK(hipMemcpy(b.W, b.hW.data(), sizeof(WT) * b.hW.size(), hipMemcpyHostToDevice));
+    const int ncopy = getenv("LAB_HOT") ? 1 : 4;
+    b.Wc.assign(1, b.W);
+    for (int c = 1; c < ncopy; ++c) {
+        WT* p;
+        CK(hipMalloc(&p, sizeof(WT) * b.hW.size()));
+        CK(hipMemcpy(p, b.W, sizeof(WT) * b.hW.size(), hipMemcpyDeviceToDevice));
+        b.Wc.push_back(p);
+    }
     CK(hipMemcpy(b.hi, b.hhi.data(), 2 * b.hhi.size(), hipMemcpyHostToDevice));
     CK(hipMemcpy(b.lo, b.hlo.data(), 2 * b.hlo.size(), hipMemcpyHostToDevice));
     PfState p{0, M};
@@ -75,7 +85,7 @@ static void make(Bufs<WT>& b, int N, int K, int M) {
 
 template <typename WT>
 static void release(Bufs<WT>& b) {
-    CK(hipFree(b.W));
+    for (auto* p : b.Wc) CK(hipFree(p));
     CK(hipFree(b.hi));
     CK(hipFree(b.lo));
     CK(hipFree(b.y));
@@ -116,7 +126,11 @@ static void run(const char* tag, Bufs<WT>& b, const Shape& sh, int M) {
     CK(hipEventCreate(&e1));
     const int iters = 20;
     CK(hipEventRecord(e0, 0));
-    for (int i = 0; i < iters; ++i) CK((launch_pgemm<PgEpiResid, Cfg, WT>(in, e, b.ps, 0)));
+    for (int i = 0; i < iters; ++i) {
+        PgIn<WT> ic = in;
+        ic.W = b.Wc[i % b.Wc.size()];
+        CK((launch_pgemm<PgEpiResid, Cfg, WT>(ic, e, b.ps, 0)));
+    }
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
     float ms = 0.0f;
@@ -133,11 +147,36 @@ static void run(const char* tag, Bufs<WT>& b, const Shape& sh, int M) {
 }
 
 #define RUN(BM, WR, S) run<PgCfg<BM, WR, S>, WT>("BM" #BM " WR" #WR " S" #S, b, sh, M)
+#define RUNP(BM, WR, S, AT) run<PgCfg<BM, WR, S, AT, true>, WT>("BM" #BM " WR" #WR " S" #S " AT" #AT " pipe", b, sh, M)
+#define RUNA(BM, WR, AT, SA) \
+    run<PgCfg<BM, WR, 2, AT, true, SA>, WT>("BM" #BM " WR" #WR " AT" #AT " pipe SA" #SA, b, sh, M)
 
 template <typename WT>
 static void sweep(const Shape& sh, int M) {
     Bufs<WT> b;
     make(b, sh.N, sh.K, M);
+    if (getenv("LAB_QUICK")) {  // the engine's tilings (prefill.h role table) and the split-ring candidates
+        if constexpr (sizeof(WT) == 2) {
+            RUNP(128, 4, 2, 2);
+            RUNA(128, 4, 2, 4);
+            RUNA(128, 4, 2, 6);
+            RUNP(64, 4, 3, 2);
+            RUNA(64, 4, 2, 4);
+            RUNA(64, 4, 2, 6);
+            RUNP(64, 2, 3, 2);
+            RUNA(64, 2, 2, 4);
+            RUNA(64, 2, 2, 6);
+            RUNA(128, 2, 2, 4);
+        } else {
+            RUNP(128, 4, 2, 2);
+            RUNP(64, 4, 2, 2);
+            RUNA(64, 4, 2, 4);
+            RUNP(64, 2, 2, 2);
+            RUNA(64, 2, 2, 4);
+        }
+        release(b);
+        return;
+    }
     if constexpr (sizeof(WT) == 2) {
         RUN(128, 2, 2);
         RUN(128, 2, 3);
