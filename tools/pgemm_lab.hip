@@ -155,24 +155,15 @@ template <typename WT>
 static void sweep(const Shape& sh, int M) {
     Bufs<WT> b;
     make(b, sh.N, sh.K, M);
-    if (getenv("LAB_QUICK")) {  // the engine's tilings (prefill.h role table) and the split-ring candidates
+    if (getenv("LAB_QUICK")) {  // the engine's tilings (prefill.h role table) and candidates
         if constexpr (sizeof(WT) == 2) {
-            RUNP(128, 4, 2, 2);
             RUNA(128, 4, 2, 4);
-            RUNA(128, 4, 2, 6);
+            RUNA(128, 2, 3, 4);
+            RUNA(128, 2, 3, 6);
+            RUNA(128, 2, 3, 8);
+            RUNP(128, 2, 2, 3);
+            RUNA(128, 4, 2, 5);
             RUNP(64, 4, 3, 2);
-            RUNA(64, 4, 2, 4);
-            RUNA(64, 4, 2, 6);
-            RUNP(64, 2, 3, 2);
-            RUNA(64, 2, 2, 4);
-            RUNA(64, 2, 2, 6);
-            RUNA(128, 2, 2, 4);
-        } else {
-            RUNP(128, 4, 2, 2);
-            RUNP(64, 4, 2, 2);
-            RUNA(64, 4, 2, 4);
-            RUNP(64, 2, 2, 2);
-            RUNA(64, 2, 2, 4);
         }
         release(b);
         return;
