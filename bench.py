@@ -550,10 +550,20 @@ def main():
         role_w = {"qkv": D * (QD + 2 * KVD), "gu": 2 * D * Il, "out": D * QD + D * Il}
         tot_w = float(sum(role_w.values()))
 
-        def bm(role, M):
+        def bm(role, M):  # chunk rows per workgroup (engine.hip StepRecorder::pg_pick)
+            if M == 32:
+                return 32
+            if role == "out":
+                return 64 if M == 256 else 32
             if a.w_dtype == "i8":
-                return 32 if M == 32 else 64 if (role == "out" or role == "gu" or M == 64) else 128
-            return 32 if (M == 32 or role == "out") else 64 if M == 64 else 128
+                if role == "gu":
+                    return 128 if M == 128 else 64
+                return 128 if M == 256 else 64
+            if M == 64 or (M == 128 and role == "qkv"):
+                return 64
+            if M == 256 and role == "gu":
+                return 64
+            return 128
         passes = sum(role_w[r] / tot_w * (M // bm(r, M)) for _, M in chunks for r in role_w)
         useful = 2.0 * params * (n - 1) * world  # whole-job flops of the projections (1 flop per MAC x 2)
         issued = 4.0 * params * sum(M for _, M in chunks) * world  # hi + lo MFMAs over the padded rows
