@@ -155,15 +155,11 @@ template <typename WT>
 static void sweep(const Shape& sh, int M) {
     Bufs<WT> b;
     make(b, sh.N, sh.K, M);
-    if (getenv("LAB_QUICK")) {  // the engine's tilings (prefill.h role table) and candidates
+    if (getenv("LAB_QUICK")) {  // the engine's fp16 tilings at M = 256 (prefill.h pg_pick)
         if constexpr (sizeof(WT) == 2) {
             RUNA(128, 4, 2, 4);
-            RUNA(128, 2, 3, 4);
-            RUNA(128, 2, 3, 6);
-            RUNA(128, 2, 3, 8);
-            RUNP(128, 2, 2, 3);
-            RUNA(128, 4, 2, 5);
             RUNP(64, 4, 3, 2);
+            RUNP(64, 2, 3, 2);
         }
         release(b);
         return;
