@@ -180,7 +180,9 @@ struct PgGeo {
     static constexpr size_t LDS = SA ? (size_t)SA * A_BYTES + (size_t)S * B_BYTES : (size_t)S * STAGE;
     static_assert(A_ROW == 128 && WPT >= 1 && NDMA % WAVES == 0, "tiling");
     static_assert(S >= 2 && (S - 1) * DPW <= 63, "ring depth (vmcnt counts 63 loads)");
-    static_assert(SA == 0 || (Cfg::PIPE && S == 2 && SA >= 2 && (A_BYTES / 1024) % WAVES == 0 &&
+    // (SA > S: A(s) must be issued in an earlier iteration than B(s), the wait below counts on it; SA == S computed
+    // wrong sums in tools/pgemm_lab)
+    static_assert(SA == 0 || (Cfg::PIPE && S == 2 && SA > S && (A_BYTES / 1024) % WAVES == 0 &&
                               (B_BYTES / 1024) % WAVES == 0 && (SA - 1) * DPA + DPB <= 63), "split rings");
     static_assert(LDS <= 160 * 1024, "LDS");
 };
