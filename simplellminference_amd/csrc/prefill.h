@@ -6,11 +6,12 @@
 //      result into fp16 hi + lo (hi = fp16(h), lo = fp16(h - hi): h to ~2^-22 relative);
 //   2. pgemm_kernel: Y[pos][row] = sum_k W[row][k] * H[pos][k] on MFMA (v_mfma_f32_16x16x32_f16), A = a 16-row
 //      weight tile, B = 16 positions' hi columns, then the same tile with the lo columns into the same fp32
-//      accumulator (W * (hi + lo)); a workgroup owns 64 weight rows x BM positions, so a weight row is read
-//      from HBM once per BM positions (the decode step reads it once per position). Operands are staged
-//      through a 3-deep LDS ring by LDS-DMA (global_load_lds_dwordx4: one 1-KiB fragment image per
-//      wave-instruction, read back conflict-free by ds_read_b128), two k-blocks in flight behind a counted
-//      vmcnt and a raw s_barrier (cdna_hip_programming.md §5 "Pipelining across barriers"); the fragment reads of
+//      accumulator (W * (hi + lo)); a workgroup owns 16 AT WR weight rows x BM positions (PgCfg), so a weight row
+//      is read from HBM once per BM positions (the decode step reads it once per position). Operands are staged
+//      through an S-deep LDS ring by LDS-DMA (global_load_lds_dwordx4: one 1-KiB fragment image per
+//      wave-instruction, read back conflict-free by ds_read_b128), S - 1 stages in flight behind a counted
+//      vmcnt and a raw s_barrier (cdna_hip_programming.md §5 "Pipelining across barriers"), or the weight images
+//      in a deeper ring of their own (PgCfg::SA, round 6); the fragment reads of
 //      the next k-block are issued ahead of the current k-block's MFMAs (two register sets, across the stage
 //      barrier too: PgCfg::PIPE, round 6, 5-20 % faster per GEMM, bit-identical sums). Fused epilogues:
 //      RoPE + K/V cache rows + q (model.cpp:52-67), residual add (:86-90, :124-128), SwiGLU (:111-115,
